@@ -1,0 +1,231 @@
+"""oracle/oracle_py.py -- TEST INFRASTRUCTURE ONLY (second, independent oracle).
+
+A pure-Python restatement of compaction.tla's Init/Next/invariants over
+immutable Python values (tuples / frozensets / None for the model value Nil),
+written separately from oracle/tlc_oracle.c so the two restatements can
+cross-check each other on small constants.  Pure-Python loops: use it only on
+state spaces of at most a few 1e5 states.  Never imported by the product.
+
+Value model (TLC values):
+  message          (id, key, value)                      ConstructMessage, compaction.tla:80-81
+  messages         tuple of messages                      compaction.tla:57
+  compactedLedgers tuple, index i-1 holds ledger i: None (Nil) or tuple of messages
+  cursor           None or (compactionHorizon, compactedTopicContext)   compaction.tla:150
+  phaseOneResult   None or (readPosition, latestForKey as sorted tuple of (key, index))  :97-98
+Counting conventions follow TLC with one worker (see tlc_oracle.c header).
+"""
+from __future__ import annotations
+
+from collections import deque
+
+P1, W, UC, UH, PER, DEL = range(6)  # compaction.tla:39-44
+ACTIONS = ("Producer", "CompactorPhaseOne", "CompactorPhaseTwoWrite",
+           "CompactorPhaseTwoUpdateContext", "CompactorPhaseTwoUpdateHorizon",
+           "CompactorPhaseTwoPersistCusror", "CompactorPhaseTwoDeleteLedger",
+           "BrokerCrash", "Consumer", "Terminating")  # Next order, compaction.tla:216-231
+
+
+class EvalError(Exception):
+    pass
+
+
+class Model:
+    def __init__(self, N=3, C=3, K=1, keys=(1, 2), values=(1, 2), retain=True,
+                 producer=False, consumer=False, ctl=2,
+                 invariants=("TypeSafe", "CompactionHorizonCorrectness"), deadlock=True):
+        self.N, self.C, self.K, self.ctl = N, C, K, ctl
+        self.keyset = sorted(set(keys) | {0})      # KeySet, compaction.tla:49
+        self.valueset = sorted(set(values) | {0})  # ValueSet, compaction.tla:50
+        self.retain, self.producer, self.consumer = retain, producer, consumer
+        self.invariants, self.deadlock = tuple(invariants), deadlock
+
+    # state = (messages, ledgers, cursor, phase, p1r, horizon, context, crash, consume)
+    def inits(self):
+        base = (None,) * self.C
+        if self.producer:
+            yield ((), base, None, P1, None, 0, 0, 0, 0)
+            return
+        per = [(k, v) for v in self.valueset for k in self.keyset]  # key fastest
+        n = len(per)
+        for idx in range(n ** self.N):
+            msgs, r = [], idx
+            for i in range(self.N):
+                k, v = per[r % n]
+                r //= n
+                msgs.append((i + 1, k, v))
+            yield (tuple(msgs), base, None, P1, None, 0, 0, 0, 0)
+
+    def max_ledger(self, led):  # MaxCompactedLedgerId, compaction.tla:103-106
+        ids = [i + 1 for i, l in enumerate(led) if l is not None]
+        return max(ids) if ids else 0
+
+    def successors(self, s):
+        """Yield (action_index, successor) in Next order; raise EvalError."""
+        msgs, led, cur, ph, p1r, hz, ctx, crash, cons = s
+        if self.producer and len(msgs) < self.N:  # Producer, :83-87
+            for k in self.keyset:
+                for v in self.valueset:
+                    yield 0, (msgs + ((len(msgs) + 1, k, v),), led, cur, ph, p1r, hz, ctx, crash, cons)
+        if ph == P1 and p1r is None and len(msgs) > 0:  # CompactorPhaseOne, :93-100
+            latest = tuple((k, max(i + 1 for i, m in enumerate(msgs) if m[1] == k))
+                           for k in sorted({m[1] for m in msgs} - {0}))
+            yield 1, (msgs, led, cur, W, (len(msgs), latest), hz, ctx, crash, cons)
+        if p1r is not None and ph == W:  # CompactorPhaseTwoWrite, :121-132
+            nid = self.max_ledger(led) + 1
+            if 1 <= nid <= self.C:
+                rp, latest = p1r
+                lf = dict(latest)
+                out = []
+                for i in range(1, rp + 1):  # CompactMessages, :107-119
+                    m = msgs[i - 1]
+                    if m[1] == 0:
+                        keep = self.retain
+                    else:
+                        if m[1] not in lf:
+                            raise EvalError("latestForKey domain")
+                        keep = (i == lf[m[1]])
+                    if keep:
+                        out.append(m)
+                nl = list(led)
+                nl[nid - 1] = tuple(out)
+                yield 2, (msgs, tuple(nl), cur, UC, p1r, hz, ctx, crash, cons)
+        if ph == UC:  # :135-139
+            yield 3, (msgs, led, cur, UH, p1r, hz, self.max_ledger(led), crash, cons)
+        if ph == UH:  # :141-145
+            if p1r is None:
+                raise EvalError("readPosition of Nil")
+            yield 4, (msgs, led, cur, PER, p1r, p1r[0], ctx, crash, cons)
+        if ph == PER:  # :147-151
+            yield 5, (msgs, led, (hz, ctx), DEL, p1r, hz, ctx, crash, cons)
+        if ph == DEL:  # :153-165
+            mx = self.max_ledger(led)
+            nl = led
+            if mx != 1:
+                old = mx - 1
+                if not 1 <= old <= self.C:
+                    raise EvalError("ledger index")
+                if led[old - 1] is not None:
+                    l2 = list(led)
+                    l2[old - 1] = None
+                    nl = tuple(l2)
+            yield 6, (msgs, nl, cur, P1, None, hz, ctx, crash, cons)
+        if crash < self.K:  # BrokerCrash, :169-182
+            h, c = cur if cur is not None else (0, 0)
+            yield 7, (msgs, led, cur, P1, None, h, c, crash + 1, cons)
+        if self.consumer:  # Consumer, :185-186
+            yield 8, s
+        if (len(msgs) == self.N and ph == W and self.max_ledger(led) == self.C
+                and (not self.consumer or cons == self.ctl)):  # Terminating, :205-214
+            yield 9, s
+
+    # ---- invariants ----
+    def ledger_at_ctx(self, s):
+        led, ctx = s[1], s[6]
+        if not 1 <= ctx <= self.C or led[ctx - 1] is None:
+            raise EvalError("compactedLedgers[ctx]")
+        return led[ctx - 1]
+
+    def inv(self, name, s):
+        msgs, led, cur, ph, p1r, hz, ctx, crash, cons = s
+        N, C = self.N, self.C
+        if name == "TypeSafe":  # :236-248
+            def ok(m):
+                return 1 <= m[0] <= N and m[1] in self.keyset and m[2] in self.valueset
+            if not all(ok(m) for m in msgs):
+                return False
+            if not all(l is None or all(ok(m) for m in l) for l in led):
+                return False
+            if p1r is not None:
+                if not all(1 <= v <= len(msgs) for _, v in p1r[1]) or not 1 <= p1r[0] <= len(msgs):
+                    return False
+            return (0 <= ph < 6 and 0 <= hz <= N and 0 <= ctx <= C and 0 <= crash <= self.K
+                    and (cur is None or (1 <= cur[0] <= N and 1 <= cur[1] <= C)))
+        if name == "CompactedLedgerLeak":  # :253
+            return sum(l is not None for l in led) <= 2
+        if name == "CompactionHorizonCorrectness":  # :259-274
+            for i in range(1, hz + 1):
+                if i > len(msgs):
+                    raise EvalError("messages[i]")
+                m = msgs[i - 1]
+                if m[1] == 0 and not self.retain:
+                    continue
+                L = self.ledger_at_ctx(s)
+                if m[1] == 0:
+                    found = any(e == m for e in L)
+                else:
+                    found = any(e[1] == m[1] and e[0] >= m[0] for e in L)
+                if not found:
+                    return False
+            return True
+        if name == "DuplicateNullKeyMessage":  # :280-294
+            if not (self.retain and ctx != 0):
+                return True
+            L = self.ledger_at_ctx(s)
+            after = msgs[hz:]
+            return all(e[1] != 0 or all(e != m for m in after) for e in L)
+        raise ValueError(name)
+
+    def check(self):
+        """TLC -workers 1 BFS. Returns a dict like tlc_oracle's JSON."""
+        seen, parent = {}, []
+        states, levels, generated = [], [], 0
+
+        def add(t, par, act):
+            if t in seen:
+                return None
+            seen[t] = len(states)
+            states.append(t)
+            parent.append((par, act))
+            return len(states) - 1
+
+        def bad(t):
+            for name in self.invariants:
+                try:
+                    if not self.inv(name, t):
+                        return ("invariant", name)
+                except EvalError:
+                    return ("invariant_error", name)
+            return None
+
+        def trace(k, extra=None):
+            out = []
+            while k is not None and k >= 0:
+                out.append((parent[k][1], states[k]))
+                k = parent[k][0]
+            out.reverse()
+            if extra:
+                out.append(extra)
+            return out
+
+        for t in self.inits():
+            generated += 1
+            k = add(t, -1, "Init")
+            if k is not None:
+                b = bad(t)
+                if b:
+                    return dict(result=b[0], invariant=b[1], generated=generated, trace=trace(k))
+        levels.append(len(states))
+        head = 0
+        while head < len(states):
+            end = len(states)
+            for p in range(head, end):
+                s = states[p]
+                n = 0
+                try:
+                    succ = list(self.successors(s))
+                except EvalError:
+                    return dict(result="action_error", generated=generated, trace=trace(p))
+                for a, t in succ:
+                    generated += 1
+                    n += 1
+                    k = add(t, p, ACTIONS[a])
+                    if k is not None:
+                        b = bad(t)
+                        if b:
+                            return dict(result=b[0], invariant=b[1], generated=generated, trace=trace(k))
+                if n == 0 and self.deadlock:
+                    return dict(result="deadlock", generated=generated, trace=trace(p))
+            head = end
+            if len(states) > end:
+                levels.append(len(states) - end)
+        return dict(result="ok", generated=generated, distinct=len(states), depth=len(levels), levels=levels)

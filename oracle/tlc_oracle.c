@@ -1,0 +1,696 @@
+/*
+ * oracle/tlc_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, sequential restatement of TLC's breadth-first safety check of
+ * /root/reference/compaction.tla (the spec) under a TLC model config.  It is
+ * the parity oracle for the HIP checker in pulsar-tlaplus_amd/: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may run it, and the
+ * product never links, loads or calls it.
+ *
+ * Independence from the product: the oracle keeps TLC *values* (message
+ * records, ledger sequences of records, the phaseOneResult record with its
+ * latestForKey function, the cursor record) in a readable struct and dedups
+ * on a canonical serialisation of those values.  It never uses the product's
+ * packed 64-bit encoding, so agreement of the two validates that encoding.
+ *
+ * Pinning: TLC itself (tla2tools.jar, Java) is absent from the reference and
+ * from this container, so the oracle is pinned by the only numbers the
+ * reference publishes, compaction.tla:23 ("the state space decrease from
+ * 253361 to 45198"), and by the hand derivations of SURVEY.md App.A
+ * (per-level counts, R(C,K) law, counterexample lengths).  TLC counting
+ * conventions it follows ([TLC-ext], not confirmable here):
+ *   - generated = initial states generated + every successor produced by
+ *     every enabled Next disjunct, stuttering self-loops included;
+ *   - invariants are checked, in cfg order, on every *new* state (inits too);
+ *   - a state with no successor at all is a deadlock (unless -deadlock);
+ *   - depth = number of BFS levels, the initial level counting as 1;
+ *   - one worker: FIFO queue, Next disjuncts in source order
+ *     (compaction.tla:216-231), first violation in generation order wins.
+ * Init enumeration order ([TLC-ext], unconfirmed): message 1 varies fastest,
+ * inside a message the key varies faster than the value (record fields
+ * id < key < value, first field fastest).  Producer successors: key outer,
+ * value inner (compaction.tla:85).
+ *
+ * Usage: tlc_oracle -N 3 -C 3 -K 1 -keys 1,2 -values 1,2 [-retain 1]
+ *        [-producer 0] [-consumer 0] [-ctl 2] [-inv TypeSafe,...]
+ *        [-nodeadlock] [-init-lo A -init-hi B] [-levels] [-quiet]
+ * Prints one JSON object on stdout.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define MAXN 8   /* MessageSentLimit */
+#define MAXC 16  /* CompactionTimesLimit */
+#define MAXK 64  /* |KeySpace| + 1 */
+
+/* ---- model constants (compaction.tla:10-18, compaction.cfg:2-11) ---- */
+static int N = 3, C = 3, K = 1, CTL = 2;
+static int RETAIN = 1, PRODUCER = 0, CONSUMER = 0, CHECK_DEADLOCK = 1;
+static int nKeySet = 0, KeySet[MAXK];     /* KeySpace \cup {NullKey}, sorted (compaction.tla:49) */
+static int nValueSet = 0, ValueSet[MAXK]; /* ValueSpace \cup {NullValue} (compaction.tla:50) */
+enum { INV_TYPESAFE, INV_LEAK, INV_HORIZON, INV_DUPNULL, N_INV_KINDS };
+static const char *INV_NAME[N_INV_KINDS] = {"TypeSafe", "CompactedLedgerLeak",
+                                            "CompactionHorizonCorrectness",
+                                            "DuplicateNullKeyMessage"};
+static int nInv = 0, Inv[8];
+
+#define NullKey 0   /* compaction.tla:47 */
+#define NullValue 0 /* compaction.tla:48 */
+
+/* compactor phases, compaction.tla:39-44 */
+enum { P_ONE, P_WRITE, P_UCTX, P_UHOR, P_PERSIST, P_DELETE };
+static const char *PHASE_NAME[6] = {
+    "Compactor_In_PhaseOne", "Compactor_In_PhaseTwoWrite",
+    "Compactor_In_PhaseTwoUpdateContext", "Compactor_In_PhaseTwoUpdateHorizon",
+    "Compactor_In_PhaseTwoPersistCusror", "Compactor_In_PhaseTwoDeleteLedger"};
+
+/* Next disjuncts in source order, compaction.tla:216-231 */
+enum { A_PRODUCER, A_PHASEONE, A_WRITE, A_UCTX, A_UHOR, A_PERSIST, A_DELETE,
+       A_CRASH, A_CONSUMER, A_TERMINATING, N_ACTIONS, A_INIT = 100 };
+static const char *ACTION_NAME[N_ACTIONS] = {
+    "Producer", "CompactorPhaseOne", "CompactorPhaseTwoWrite",
+    "CompactorPhaseTwoUpdateContext", "CompactorPhaseTwoUpdateHorizon",
+    "CompactorPhaseTwoPersistCusror", "CompactorPhaseTwoDeleteLedger",
+    "BrokerCrash", "Consumer", "Terminating"};
+
+/* ---- TLC values of one state (compaction.tla:57-70) ---- */
+typedef struct { int id, key, value; } Msg; /* ConstructMessage, compaction.tla:80-81 */
+
+typedef struct {
+  int nmsg; Msg msgs[MAXN];                 /* messages: Seq(Msg) */
+  int led_nil[MAXC + 1];                    /* compactedLedgers[i] = Nil ? (1-based) */
+  int led_len[MAXC + 1]; Msg led[MAXC + 1][MAXN];
+  int cur_nil, cur_h, cur_c;                /* cursor: Nil or [compactionHorizon, compactedTopicContext] */
+  int phase;                                /* compactorState */
+  int p1r_nil, p1r_rp;                      /* phaseOneResult: Nil or [readPosition, latestForKey] */
+  int p1r_n, p1r_dom[MAXK], p1r_val[MAXK];  /* latestForKey as sorted (key |-> index) pairs */
+  int hz, ctx, crash, consume;              /* compactionHorizon, compactedTopicContext, crashTimes, consumeTimes */
+} St;
+
+/* evaluation outcome of an action / invariant */
+enum { EV_FALSE = 0, EV_TRUE = 1, EV_ERROR = -1 };
+static char g_errmsg[256];
+
+/* ---------------- canonical serialisation + FP set ---------------- */
+typedef struct { int32_t *v; size_t n, cap; } IVec;
+static void iv_push(IVec *a, int32_t x) {
+  if (a->n == a->cap) { a->cap = a->cap ? a->cap * 2 : 1 << 20; a->v = realloc(a->v, a->cap * sizeof(int32_t)); if (!a->v) { fprintf(stderr, "oom\n"); exit(3); } }
+  a->v[a->n++] = x;
+}
+
+static int serialize(const St *s, int32_t *o) {
+  int n = 0;
+  o[n++] = s->nmsg;
+  for (int i = 0; i < s->nmsg; i++) { o[n++] = s->msgs[i].id; o[n++] = s->msgs[i].key; o[n++] = s->msgs[i].value; }
+  for (int j = 1; j <= C; j++) {
+    if (s->led_nil[j]) { o[n++] = -1; continue; }
+    o[n++] = s->led_len[j];
+    for (int e = 0; e < s->led_len[j]; e++) { o[n++] = s->led[j][e].id; o[n++] = s->led[j][e].key; o[n++] = s->led[j][e].value; }
+  }
+  if (s->cur_nil) o[n++] = -1; else { o[n++] = s->cur_h; o[n++] = s->cur_c; }
+  o[n++] = s->phase;
+  if (s->p1r_nil) o[n++] = -1;
+  else {
+    o[n++] = s->p1r_rp; o[n++] = s->p1r_n;
+    for (int i = 0; i < s->p1r_n; i++) { o[n++] = s->p1r_dom[i]; o[n++] = s->p1r_val[i]; }
+  }
+  o[n++] = s->hz; o[n++] = s->ctx; o[n++] = s->crash; o[n++] = s->consume;
+  return n;
+}
+
+static void deserialize(const int32_t *o, St *s) {
+  memset(s, 0, sizeof *s);
+  int n = 0;
+  s->nmsg = o[n++];
+  for (int i = 0; i < s->nmsg; i++) { s->msgs[i].id = o[n++]; s->msgs[i].key = o[n++]; s->msgs[i].value = o[n++]; }
+  for (int j = 1; j <= C; j++) {
+    int l = o[n++];
+    if (l < 0) { s->led_nil[j] = 1; continue; }
+    s->led_len[j] = l;
+    for (int e = 0; e < l; e++) { s->led[j][e].id = o[n++]; s->led[j][e].key = o[n++]; s->led[j][e].value = o[n++]; }
+  }
+  int h = o[n++];
+  if (h < 0) s->cur_nil = 1; else { s->cur_h = h; s->cur_c = o[n++]; }
+  s->phase = o[n++];
+  int rp = o[n++];
+  if (rp < 0) s->p1r_nil = 1;
+  else {
+    s->p1r_rp = rp; s->p1r_n = o[n++];
+    for (int i = 0; i < s->p1r_n; i++) { s->p1r_dom[i] = o[n++]; s->p1r_val[i] = o[n++]; }
+  }
+  s->hz = o[n++]; s->ctx = o[n++]; s->crash = o[n++]; s->consume = o[n++];
+}
+
+static uint64_t hash_ints(const int32_t *o, int n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+  for (int i = 0; i < n; i++) {
+    h ^= (uint32_t)o[i];
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 32;
+  }
+  return h;
+}
+
+/* state store: serialised states in discovery (= BFS queue) order */
+static IVec arena;                 /* concatenated serialisations */
+static uint64_t *st_off = NULL;    /* offset of state k in arena */
+static int32_t *st_len = NULL;
+static int64_t *st_parent = NULL;  /* parent state index, -1 for initial states */
+static int8_t *st_action = NULL;   /* action that first discovered it */
+static uint64_t n_states = 0, st_cap = 0;
+static uint64_t *fp_tab = NULL;    /* open addressing: 0 empty, else state index + 1 */
+static uint64_t fp_mask = 0;
+
+static void fp_grow(void);
+static void store_reserve(void) {
+  if (n_states < st_cap) return;
+  st_cap = st_cap ? st_cap * 2 : 1 << 16;
+  st_off = realloc(st_off, st_cap * sizeof *st_off);
+  st_len = realloc(st_len, st_cap * sizeof *st_len);
+  st_parent = realloc(st_parent, st_cap * sizeof *st_parent);
+  st_action = realloc(st_action, st_cap * sizeof *st_action);
+  if (!st_off || !st_len || !st_parent || !st_action) { fprintf(stderr, "oom\n"); exit(3); }
+}
+
+static int same(uint64_t k, const int32_t *o, int n) {
+  return st_len[k] == n && memcmp(arena.v + st_off[k], o, n * sizeof(int32_t)) == 0;
+}
+
+/* FPSet.put: returns 1 if the state is new (and stores it), 0 if seen. */
+static int fp_put(const St *s, int64_t parent, int action, uint64_t *idx_out) {
+  int32_t buf[1024];
+  int n = serialize(s, buf);
+  if ((n_states + 1) * 2 > fp_mask + 1) fp_grow();
+  uint64_t h = hash_ints(buf, n) & fp_mask;
+  for (;;) {
+    uint64_t e = fp_tab[h];
+    if (e == 0) break;
+    if (same(e - 1, buf, n)) { if (idx_out) *idx_out = e - 1; return 0; }
+    h = (h + 1) & fp_mask;
+  }
+  store_reserve();
+  st_off[n_states] = arena.n; st_len[n_states] = n;
+  st_parent[n_states] = parent; st_action[n_states] = (int8_t)action;
+  for (int i = 0; i < n; i++) iv_push(&arena, buf[i]);
+  fp_tab[h] = n_states + 1;
+  if (idx_out) *idx_out = n_states;
+  n_states++;
+  return 1;
+}
+
+static void fp_grow(void) {
+  uint64_t ncap = fp_mask ? (fp_mask + 1) * 2 : 1 << 16;
+  uint64_t *nt = calloc(ncap, sizeof *nt);
+  if (!nt) { fprintf(stderr, "oom\n"); exit(3); }
+  for (uint64_t k = 0; k < n_states; k++) {
+    uint64_t h = hash_ints(arena.v + st_off[k], st_len[k]) & (ncap - 1);
+    while (nt[h]) h = (h + 1) & (ncap - 1);
+    nt[h] = k + 1;
+  }
+  free(fp_tab); fp_tab = nt; fp_mask = ncap - 1;
+}
+
+static void load_state(uint64_t k, St *s) { deserialize(arena.v + st_off[k], s); }
+
+/* ---------------- operators of the spec ---------------- */
+
+/* MaxCompactedLedgerId, compaction.tla:103-106 */
+static int MaxCompactedLedgerId(const St *s) {
+  int m = 0;
+  for (int i = 1; i <= C; i++) if (!s->led_nil[i]) m = i;
+  return m;
+}
+
+/* latestForKey[key] lookup (the function built in CompactorPhaseOne) */
+static int latest_for_key(const St *s, int key, int *ok) {
+  for (int i = 0; i < s->p1r_n; i++) if (s->p1r_dom[i] == key) { *ok = 1; return s->p1r_val[i]; }
+  *ok = 0; return 0;
+}
+
+/* Producer, compaction.tla:83-87.  Appends every (key, value) pair. */
+static int act_producer(const St *s, St *out, int *nout) {
+  *nout = 0;
+  if (!(s->nmsg < N)) return EV_FALSE;
+  for (int ki = 0; ki < nKeySet; ki++)
+    for (int vi = 0; vi < nValueSet; vi++) {
+      St t = *s;
+      t.msgs[t.nmsg].id = s->nmsg + 1;
+      t.msgs[t.nmsg].key = KeySet[ki];
+      t.msgs[t.nmsg].value = ValueSet[vi];
+      t.nmsg++;
+      out[(*nout)++] = t;
+    }
+  return EV_TRUE;
+}
+
+/* CompactorPhaseOne, compaction.tla:93-100 (Max :91, GetKeys :92) */
+static int act_phase_one(const St *s, St *t) {
+  if (s->phase != P_ONE) return EV_FALSE;
+  if (!s->p1r_nil) return EV_FALSE;
+  if (!(s->nmsg > 0)) return EV_FALSE;
+  *t = *s;
+  t->p1r_nil = 0;
+  t->p1r_rp = s->nmsg;
+  /* latestForKey == [key \in GetKeys(messages) |-> Max({i : messages[i].key = key})];
+     domain enumerated in sorted key order (a TLC set is normalised). */
+  t->p1r_n = 0;
+  for (int ki = 0; ki < nKeySet; ki++) {
+    int key = KeySet[ki];
+    if (key == NullKey) continue; /* GetKeys removes NullKey */
+    int mx = 0, present = 0;
+    for (int i = 1; i <= s->nmsg; i++)
+      if (s->msgs[i - 1].key == key) { present = 1; if (i > mx) mx = i; }
+    if (present) { t->p1r_dom[t->p1r_n] = key; t->p1r_val[t->p1r_n] = mx; t->p1r_n++; }
+  }
+  t->phase = P_WRITE;
+  return EV_TRUE;
+}
+
+/* CompactMessages, compaction.tla:107-119: the function over 1..readPosition
+   (Nil for dropped entries), then SelectSeq(_, LAMBDA i: i # Nil). */
+static int CompactMessages(const St *s, Msg *res, int *nres) {
+  *nres = 0;
+  for (int i = 1; i <= s->p1r_rp; i++) {
+    if (i > s->nmsg) { snprintf(g_errmsg, sizeof g_errmsg, "messages[%d] out of domain", i); return EV_ERROR; }
+    const Msg *m = &s->msgs[i - 1];
+    int keep;
+    if (m->key == NullKey) keep = RETAIN;
+    else {
+      int ok, l = latest_for_key(s, m->key, &ok);
+      if (!ok) { snprintf(g_errmsg, sizeof g_errmsg, "latestForKey[%d] out of domain", m->key); return EV_ERROR; }
+      keep = (i == l);
+    }
+    if (keep) res[(*nres)++] = *m;
+  }
+  return EV_TRUE;
+}
+
+/* CompactorPhaseTwoWrite, compaction.tla:121-132 */
+static int act_write(const St *s, St *t) {
+  if (s->p1r_nil) return EV_FALSE;
+  if (s->phase != P_WRITE) return EV_FALSE;
+  int newId = MaxCompactedLedgerId(s) + 1;
+  if (!(newId >= 1 && newId <= C)) return EV_FALSE;
+  /* the LET-bound compactedMessages is evaluated only once the guard holds */
+  Msg cm[MAXN]; int ncm;
+  if (CompactMessages(s, cm, &ncm) == EV_ERROR) return EV_ERROR;
+  *t = *s;
+  t->led_nil[newId] = 0;
+  t->led_len[newId] = ncm;
+  memcpy(t->led[newId], cm, sizeof(Msg) * ncm);
+  t->phase = P_UCTX;
+  return EV_TRUE;
+}
+
+/* CompactorPhaseTwoUpdateContext, compaction.tla:135-139 */
+static int act_update_context(const St *s, St *t) {
+  if (s->phase != P_UCTX) return EV_FALSE;
+  *t = *s;
+  t->phase = P_UHOR;
+  t->ctx = MaxCompactedLedgerId(s);
+  return EV_TRUE;
+}
+
+/* CompactorPhaseTwoUpdateHorizon, compaction.tla:141-145 */
+static int act_update_horizon(const St *s, St *t) {
+  if (s->phase != P_UHOR) return EV_FALSE;
+  if (s->p1r_nil) { snprintf(g_errmsg, sizeof g_errmsg, "field readPosition of Nil"); return EV_ERROR; }
+  *t = *s;
+  t->phase = P_PERSIST;
+  t->hz = s->p1r_rp;
+  return EV_TRUE;
+}
+
+/* CompactorPhaseTwoPersistCusror, compaction.tla:147-151 */
+static int act_persist(const St *s, St *t) {
+  if (s->phase != P_PERSIST) return EV_FALSE;
+  *t = *s;
+  t->phase = P_DELETE;
+  t->cur_nil = 0; t->cur_h = s->hz; t->cur_c = s->ctx;
+  return EV_TRUE;
+}
+
+/* CompactorPhaseTwoDeleteLedger, compaction.tla:153-165 */
+static int act_delete(const St *s, St *t) {
+  if (s->phase != P_DELETE) return EV_FALSE;
+  *t = *s;
+  t->phase = P_ONE;
+  t->p1r_nil = 1; t->p1r_rp = 0; t->p1r_n = 0;
+  int maxId = MaxCompactedLedgerId(s);
+  if (maxId == 1) return EV_TRUE; /* oldCompactedLedgerId = Nil: UNCHANGED */
+  int old = maxId - 1;
+  if (old < 1 || old > C) { snprintf(g_errmsg, sizeof g_errmsg, "compactedLedgers[%d] out of domain", old); return EV_ERROR; }
+  if (s->led_nil[old]) return EV_TRUE;
+  t->led_nil[old] = 1; t->led_len[old] = 0;
+  memset(t->led[old], 0, sizeof t->led[old]);
+  return EV_TRUE;
+}
+
+/* BrokerCrash, compaction.tla:169-182 */
+static int act_crash(const St *s, St *t) {
+  if (!(s->crash < K)) return EV_FALSE;
+  *t = *s;
+  t->crash = s->crash + 1;
+  t->phase = P_ONE;
+  t->p1r_nil = 1; t->p1r_rp = 0; t->p1r_n = 0;
+  if (!s->cur_nil) { t->hz = s->cur_h; t->ctx = s->cur_c; }
+  else { t->hz = 0; t->ctx = 0; }
+  return EV_TRUE;
+}
+
+/* Terminating, compaction.tla:205-214 */
+static int enabled_terminating(const St *s) {
+  return s->nmsg == N && s->phase == P_WRITE && MaxCompactedLedgerId(s) == C &&
+         (!CONSUMER || s->consume == CTL);
+}
+
+/* ---------------- invariants ---------------- */
+
+static int msg_in_space(const Msg *m) { /* [id: 1..N, key: KeySet, value: ValueSet] */
+  int ok = m->id >= 1 && m->id <= N, k = 0, v = 0;
+  for (int i = 0; i < nKeySet; i++) if (KeySet[i] == m->key) k = 1;
+  for (int i = 0; i < nValueSet; i++) if (ValueSet[i] == m->value) v = 1;
+  return ok && k && v;
+}
+
+/* TypeSafe, compaction.tla:236-248 */
+static int inv_typesafe(const St *s) {
+  for (int i = 0; i < s->nmsg; i++) if (!msg_in_space(&s->msgs[i])) return EV_FALSE;
+  for (int i = 1; i <= C; i++)
+    if (!s->led_nil[i])
+      for (int j = 0; j < s->led_len[i]; j++) if (!msg_in_space(&s->led[i][j])) return EV_FALSE;
+  if (!s->p1r_nil) {
+    for (int i = 0; i < s->p1r_n; i++) if (!(s->p1r_val[i] >= 1 && s->p1r_val[i] <= s->nmsg)) return EV_FALSE;
+    if (!(s->p1r_rp >= 1 && s->p1r_rp <= s->nmsg)) return EV_FALSE;
+  }
+  if (!(s->phase >= 0 && s->phase < 6)) return EV_FALSE;
+  if (!(s->hz >= 0 && s->hz <= N)) return EV_FALSE;
+  if (!(s->ctx >= 0 && s->ctx <= C)) return EV_FALSE;
+  if (!(s->crash >= 0 && s->crash <= K)) return EV_FALSE;
+  if (!s->cur_nil && !(s->cur_h >= 1 && s->cur_h <= N && s->cur_c >= 1 && s->cur_c <= C)) return EV_FALSE;
+  return EV_TRUE;
+}
+
+/* CompactedLedgerLeak, compaction.tla:253 */
+static int inv_leak(const St *s) {
+  int n = 0;
+  for (int i = 1; i <= C; i++) if (!s->led_nil[i]) n++;
+  return n <= 2 ? EV_TRUE : EV_FALSE;
+}
+
+static int msg_eq(const Msg *a, const Msg *b) { return a->id == b->id && a->key == b->key && a->value == b->value; }
+
+/* the LET-bound compactedLedger == compactedLedgers[compactedTopicContext],
+   evaluated lazily (TLC evaluates a LET definition on first use) and then
+   Len(.) of it: errors on an out-of-domain index or on Nil. */
+static int ledger_at_ctx(const St *s, int *idx) {
+  if (s->ctx < 1 || s->ctx > C) { snprintf(g_errmsg, sizeof g_errmsg, "compactedLedgers[%d] out of domain", s->ctx); return EV_ERROR; }
+  if (s->led_nil[s->ctx]) { snprintf(g_errmsg, sizeof g_errmsg, "Len(Nil)"); return EV_ERROR; }
+  *idx = s->ctx;
+  return EV_TRUE;
+}
+
+/* CompactionHorizonCorrectness, compaction.tla:259-274 */
+static int inv_horizon(const St *s) {
+  for (int i = 1; i <= s->hz; i++) { /* \A i \in 1..Len(messagesBeforeHorizon), in order */
+    if (i > s->nmsg) { snprintf(g_errmsg, sizeof g_errmsg, "messages[%d] out of domain", i); return EV_ERROR; }
+    const Msg *mi = &s->msgs[i - 1];
+    int isNil = (mi->key == NullKey) && !RETAIN; /* messagesBeforeHorizon[i] */
+    if (isNil) continue;                          /* RetainNullKey => ... is TRUE */
+    int L;
+    if (ledger_at_ctx(s, &L) == EV_ERROR) return EV_ERROR;
+    int found = 0;
+    for (int j = 0; j < s->led_len[L] && !found; j++) {
+      const Msg *e = &s->led[L][j];
+      if (mi->key == NullKey) found = msg_eq(e, mi);          /* RETAIN: exact record match */
+      else found = (e->key == mi->key && e->id >= mi->id);
+    }
+    if (!found) return EV_FALSE;
+  }
+  return EV_TRUE;
+}
+
+/* DuplicateNullKeyMessage, compaction.tla:280-294 */
+static int inv_dupnull(const St *s) {
+  if (!(RETAIN && s->ctx != 0)) return EV_TRUE;
+  int L;
+  if (ledger_at_ctx(s, &L) == EV_ERROR) return EV_ERROR;
+  for (int i = 0; i < s->led_len[L]; i++) {
+    const Msg *e = &s->led[L][i];
+    if (e->key != NullKey) continue;
+    for (int j = s->hz + 1; j <= s->nmsg; j++) {
+      const Msg *mj = &s->msgs[j - 1]; /* messagesAfterHorizon[j] (RETAIN: the message itself) */
+      if (msg_eq(e, mj)) return EV_FALSE;
+    }
+  }
+  return EV_TRUE;
+}
+
+static int eval_inv(int kind, const St *s) {
+  switch (kind) {
+    case INV_TYPESAFE: return inv_typesafe(s);
+    case INV_LEAK: return inv_leak(s);
+    case INV_HORIZON: return inv_horizon(s);
+    case INV_DUPNULL: return inv_dupnull(s);
+  }
+  return EV_ERROR;
+}
+
+/* ---------------- TLC value printing ---------------- */
+static void p_msg(FILE *f, const Msg *m) { fprintf(f, "[id |-> %d, key |-> %d, value |-> %d]", m->id, m->key, m->value); }
+static void p_seq(FILE *f, const Msg *a, int n) {
+  fprintf(f, "<<");
+  for (int i = 0; i < n; i++) { if (i) fprintf(f, ", "); p_msg(f, &a[i]); }
+  fprintf(f, ">>");
+}
+static void print_state_json(FILE *f, const St *s) {
+  /* one string, lines "/\\ var = value" in declaration order (compaction.tla:57-70) */
+  fprintf(f, "\"/\\\\ messages = ");
+  p_seq(f, s->msgs, s->nmsg);
+  fprintf(f, "\\n/\\\\ compactedLedgers = <<");
+  for (int j = 1; j <= C; j++) {
+    if (j > 1) fprintf(f, ", ");
+    if (s->led_nil[j]) fprintf(f, "Nil"); else p_seq(f, s->led[j], s->led_len[j]);
+  }
+  fprintf(f, ">>\\n/\\\\ cursor = ");
+  if (s->cur_nil) fprintf(f, "Nil");
+  else fprintf(f, "[compactedTopicContext |-> %d, compactionHorizon |-> %d]", s->cur_c, s->cur_h);
+  fprintf(f, "\\n/\\\\ compactorState = %s", PHASE_NAME[s->phase]);
+  fprintf(f, "\\n/\\\\ phaseOneResult = ");
+  if (s->p1r_nil) fprintf(f, "Nil");
+  else {
+    fprintf(f, "[latestForKey |-> ");
+    int tuple = 1;
+    for (int i = 0; i < s->p1r_n; i++) if (s->p1r_dom[i] != i + 1) tuple = 0;
+    if (tuple) {
+      fprintf(f, "<<");
+      for (int i = 0; i < s->p1r_n; i++) fprintf(f, "%s%d", i ? ", " : "", s->p1r_val[i]);
+      fprintf(f, ">>");
+    } else {
+      fprintf(f, "(");
+      for (int i = 0; i < s->p1r_n; i++) fprintf(f, "%s%d :> %d", i ? " @@ " : "", s->p1r_dom[i], s->p1r_val[i]);
+      fprintf(f, ")");
+    }
+    fprintf(f, ", readPosition |-> %d]", s->p1r_rp);
+  }
+  fprintf(f, "\\n/\\\\ compactionHorizon = %d", s->hz);
+  fprintf(f, "\\n/\\\\ compactedTopicContext = %d", s->ctx);
+  fprintf(f, "\\n/\\\\ crashTimes = %d", s->crash);
+  fprintf(f, "\\n/\\\\ consumeTimes = %d\"", s->consume);
+}
+
+/* ---------------- BFS (TLC ModelChecker with one worker) ---------------- */
+enum { R_OK, R_INV, R_INV_ERROR, R_DEADLOCK, R_ACTION_ERROR };
+static const char *RESULT_NAME[] = {"ok", "invariant", "invariant_error", "deadlock", "action_error"};
+
+static void init_state(St *s) {
+  /* compaction.tla:188-202 (messages assigned by the caller) */
+  memset(s, 0, sizeof *s);
+  for (int j = 1; j <= C; j++) s->led_nil[j] = 1;
+  s->p1r_nil = 1;
+  s->phase = P_ONE;
+  s->cur_nil = 1;
+}
+
+static int parse_list(const char *a, int *out, int max) {
+  int n = 0;
+  const char *p = a;
+  while (*p && n < max) {
+    out[n++] = (int)strtol(p, (char **)&p, 10);
+    if (*p == ',') p++;
+  }
+  return n;
+}
+
+static int cmp_int(const void *a, const void *b) { return (*(const int *)a > *(const int *)b) - (*(const int *)a < *(const int *)b); }
+
+int main(int argc, char **argv) {
+  int keys[MAXK], nkeys = 0, vals[MAXK], nvals = 0;
+  long long init_lo = 0, init_hi = -1;
+  int print_levels = 0, want_trace = 1;
+  char invs[512] = "TypeSafe,CompactionHorizonCorrectness";
+  for (int i = 1; i < argc; i++) {
+    const char *a = argv[i];
+#define NEXT (i + 1 < argc ? argv[++i] : "")
+    if (!strcmp(a, "-N")) N = atoi(NEXT);
+    else if (!strcmp(a, "-C")) C = atoi(NEXT);
+    else if (!strcmp(a, "-K")) K = atoi(NEXT);
+    else if (!strcmp(a, "-ctl")) CTL = atoi(NEXT);
+    else if (!strcmp(a, "-keys")) nkeys = parse_list(NEXT, keys, MAXK - 1);
+    else if (!strcmp(a, "-values")) nvals = parse_list(NEXT, vals, MAXK - 1);
+    else if (!strcmp(a, "-retain")) RETAIN = atoi(NEXT);
+    else if (!strcmp(a, "-producer")) PRODUCER = atoi(NEXT);
+    else if (!strcmp(a, "-consumer")) CONSUMER = atoi(NEXT);
+    else if (!strcmp(a, "-nodeadlock")) CHECK_DEADLOCK = 0;
+    else if (!strcmp(a, "-inv")) snprintf(invs, sizeof invs, "%s", NEXT);
+    else if (!strcmp(a, "-init-lo")) init_lo = atoll(NEXT);
+    else if (!strcmp(a, "-init-hi")) init_hi = atoll(NEXT);
+    else if (!strcmp(a, "-levels")) print_levels = 1;
+    else if (!strcmp(a, "-notrace")) want_trace = 0;
+    else { fprintf(stderr, "unknown arg %s\n", a); return 2; }
+  }
+  if (N < 0 || N > MAXN || C < 0 || C > MAXC || K < 0) { fprintf(stderr, "constants out of oracle range\n"); return 2; }
+  /* KeySet / ValueSet, normalised (sorted) like a TLC set */
+  KeySet[nKeySet++] = NullKey;
+  for (int i = 0; i < nkeys; i++) if (keys[i] != NullKey) KeySet[nKeySet++] = keys[i];
+  qsort(KeySet, nKeySet, sizeof(int), cmp_int);
+  ValueSet[nValueSet++] = NullValue;
+  for (int i = 0; i < nvals; i++) if (vals[i] != NullValue) ValueSet[nValueSet++] = vals[i];
+  qsort(ValueSet, nValueSet, sizeof(int), cmp_int);
+  if (strlen(invs)) {
+    char tmp[512]; snprintf(tmp, sizeof tmp, "%s", invs);
+    for (char *tok = strtok(tmp, ","); tok; tok = strtok(NULL, ",")) {
+      int k = -1;
+      for (int j = 0; j < N_INV_KINDS; j++) if (!strcmp(tok, INV_NAME[j])) k = j;
+      if (k < 0) { fprintf(stderr, "unknown invariant %s\n", tok); return 2; }
+      Inv[nInv++] = k;
+    }
+  }
+
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+
+  uint64_t generated = 0;
+  int result = R_OK, bad_inv = -1;
+  int64_t bad_parent = -1; int bad_action = -1; St bad_state; memset(&bad_state, 0, sizeof bad_state);
+  uint64_t level_start[4096]; int nlevels = 0;
+  fp_grow();
+
+  /* ---- Init (compaction.tla:188-202) ---- */
+  level_start[0] = 0;
+  {
+    long long total = 1;
+    if (!PRODUCER) for (int i = 0; i < N; i++) total *= (long long)(nKeySet * nValueSet);
+    if (init_hi < 0 || init_hi > total) init_hi = total;
+    for (long long idx = init_lo; idx < init_hi && result == R_OK; idx++) {
+      St s; init_state(&s);
+      if (!PRODUCER) {
+        /* messages \in {msgs \in [1..N -> [id, key, value]] : \A i: msgs[i].id = i} */
+        long long r = idx;
+        s.nmsg = N;
+        for (int i = 0; i < N; i++) {
+          int d = (int)(r % (nKeySet * nValueSet)); r /= (nKeySet * nValueSet);
+          s.msgs[i].id = i + 1;
+          s.msgs[i].key = KeySet[d % nKeySet];
+          s.msgs[i].value = ValueSet[d / nKeySet];
+        }
+      }
+      generated++;
+      uint64_t k;
+      if (fp_put(&s, -1, A_INIT, &k)) {
+        for (int q = 0; q < nInv; q++) {
+          int v = eval_inv(Inv[q], &s);
+          if (v != EV_TRUE) { result = v == EV_ERROR ? R_INV_ERROR : R_INV; bad_inv = Inv[q]; bad_parent = -2; bad_state = s; bad_action = A_INIT; break; }
+        }
+      }
+    }
+  }
+  uint64_t n_init = n_states;
+  nlevels = 1;
+  level_start[1] = n_states;
+
+  /* ---- BFS: FIFO over the store (store order == queue order) ---- */
+  static St succ[MAXK * MAXK + 16];
+  uint64_t head = 0;
+  while (result == R_OK && head < n_states) {
+    uint64_t lvl_end = n_states; /* current level [head, lvl_end) */
+    for (; head < lvl_end && result == R_OK; head++) {
+      St s; load_state(head, &s);
+      int nsucc = 0;
+      /* Next, compaction.tla:216-231: disjuncts in source order */
+      for (int a = 0; a < N_ACTIONS && result == R_OK; a++) {
+        int cnt = 0, rc = EV_FALSE;
+        St *out = succ;
+        switch (a) {
+          case A_PRODUCER: if (PRODUCER) rc = act_producer(&s, out, &cnt); break;
+          case A_PHASEONE: rc = act_phase_one(&s, out); cnt = rc == EV_TRUE; break;
+          case A_WRITE: rc = act_write(&s, out); cnt = rc == EV_TRUE; break;
+          case A_UCTX: rc = act_update_context(&s, out); cnt = rc == EV_TRUE; break;
+          case A_UHOR: rc = act_update_horizon(&s, out); cnt = rc == EV_TRUE; break;
+          case A_PERSIST: rc = act_persist(&s, out); cnt = rc == EV_TRUE; break;
+          case A_DELETE: rc = act_delete(&s, out); cnt = rc == EV_TRUE; break;
+          case A_CRASH: rc = act_crash(&s, out); cnt = rc == EV_TRUE; break;
+          case A_CONSUMER: if (CONSUMER) { out[0] = s; cnt = 1; } break; /* UNCHANGED vars, :185-186 */
+          case A_TERMINATING: if (enabled_terminating(&s)) { out[0] = s; cnt = 1; } break;
+        }
+        if (rc == EV_ERROR) { result = R_ACTION_ERROR; bad_parent = (int64_t)head; bad_action = a; break; }
+        for (int j = 0; j < cnt && result == R_OK; j++) {
+          generated++; nsucc++;
+          uint64_t k;
+          if (fp_put(&out[j], (int64_t)head, a, &k)) {
+            for (int q = 0; q < nInv; q++) {
+              int v = eval_inv(Inv[q], &out[j]);
+              if (v != EV_TRUE) { result = v == EV_ERROR ? R_INV_ERROR : R_INV; bad_inv = Inv[q]; bad_parent = (int64_t)head; bad_action = a; bad_state = out[j]; break; }
+            }
+          }
+        }
+      }
+      if (result == R_OK && nsucc == 0 && CHECK_DEADLOCK) { result = R_DEADLOCK; bad_parent = (int64_t)head; bad_state = s; }
+    }
+    if (n_states > lvl_end) { nlevels++; level_start[nlevels] = n_states; }
+  }
+
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  double secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+
+  printf("{\"result\": \"%s\", \"generated\": %llu, \"distinct\": %llu, \"init\": %llu, \"depth\": %d, \"seconds\": %.6f",
+         RESULT_NAME[result], (unsigned long long)generated, (unsigned long long)n_states,
+         (unsigned long long)n_init, nlevels, secs);
+  if (result == R_OK) printf(", \"left_on_queue\": 0");
+  if (print_levels) {
+    printf(", \"levels\": [");
+    for (int l = 0; l < nlevels; l++) printf("%s%llu", l ? ", " : "", (unsigned long long)(level_start[l + 1] - level_start[l]));
+    printf("]");
+  }
+  if (result != R_OK) {
+    if (bad_inv >= 0) printf(", \"invariant\": \"%s\"", INV_NAME[bad_inv]);
+    if (result == R_ACTION_ERROR) printf(", \"action\": \"%s\", \"error\": \"%s\"", ACTION_NAME[bad_action], g_errmsg);
+    if (result == R_INV_ERROR) printf(", \"error\": \"%s\"", g_errmsg);
+    if (want_trace) {
+      /* TLCTrace: walk parent pointers back to an initial state */
+      int64_t chain[4096]; int nc = 0;
+      for (int64_t k = bad_parent; k >= 0; k = st_parent[k]) chain[nc++] = k;
+      printf(", \"trace\": [");
+      int first = 1;
+      for (int i = nc - 1; i >= 0; i--) {
+        St s; load_state((uint64_t)chain[i], &s);
+        int a = st_action[chain[i]];
+        printf("%s{\"action\": \"%s\", \"state\": ", first ? "" : ", ", a == A_INIT ? "Init" : ACTION_NAME[a]);
+        print_state_json(stdout, &s);
+        printf("}");
+        first = 0;
+      }
+      if (result == R_INV || result == R_INV_ERROR) {
+        printf("%s{\"action\": \"%s\", \"state\": ", first ? "" : ", ", bad_action == A_INIT ? "Init" : ACTION_NAME[bad_action]);
+        print_state_json(stdout, &bad_state);
+        printf("}");
+      }
+      printf("]");
+    }
+  }
+  printf("}\n");
+  return 0;
+}
