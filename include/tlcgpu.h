@@ -1,0 +1,186 @@
+/*
+ * include/tlcgpu.h -- C ABI of libtlcgpu.so, the MI355X (gfx950) BFS safety
+ * checker for the Pulsar topic-compaction spec (/root/reference/compaction.tla).
+ *
+ * This is the drop-in boundary: the entry points are the calls TLC's model
+ * checker core makes on the path the HIP kernels replace.  TLC (tla2tools.jar)
+ * is not part of the reference repo (its .gitignore:3 ignores *.jar), so the
+ * TLC classes are cited by name; the spec lines are cited as file:line.
+ *
+ *   tlcg_check_model  <- ModelChecker.checkAssumptions: the ASSUME of
+ *                        compaction.tla:25-35 on the bound constants
+ *   tlcg_create       <- new ModelChecker(...) + FPSet / StateQueue / TLCTrace
+ *                        allocation (tlc2.tool.ModelChecker, tlc2.tool.fp.FPSet)
+ *   tlcg_init         <- ModelChecker.doInit: Init, compaction.tla:188-202,
+ *                        FPSet.put + invariant check of each initial state
+ *   tlcg_step_level   <- one BFS level of tlc2.tool.Worker.run: Next
+ *                        (compaction.tla:216-231), fingerprint, FPSet.put,
+ *                        invariants (compaction.cfg:25-31), enqueue, deadlock
+ *   tlcg_run          <- ModelChecker.runTLC (levels until done or error)
+ *   tlcg_trace        <- TLCTrace.getTrace (parent-pointer walk)
+ *   tlcg_decode       <- TLCStateMut.toString (TLC value syntax)
+ *   tlcg_expand / tlcg_outbox / tlcg_inbox / tlcg_absorb / tlcg_end_level
+ *                     <- the per-level exchange of a fingerprint-partitioned
+ *                        FPSet (TLC's distributed tlc2.tool.fp.FPSetManager),
+ *                        one rank per GPU
+ *
+ * Conventions: plain C, no exceptions cross the ABI, buffers are owned by the
+ * caller, one host thread per context.  A negative return is an error whose
+ * text tlcg_last_error() returns.  Device pointers handed out by
+ * tlcg_outbox/tlcg_inbox are valid until the next call on the context.
+ */
+#ifndef TLCGPU_H
+#define TLCGPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TLCG_ABI_VERSION 1
+#define TLCG_MAX_SET 63 /* largest KeySpace / ValueSpace */
+#define TLCG_MAX_INV 8
+
+/* invariants the spec defines (compaction.tla:236,253,259,280) */
+enum {
+  TLCG_INV_TYPESAFE = 0,            /* TypeSafe */
+  TLCG_INV_COMPACTED_LEDGER_LEAK = 1, /* CompactedLedgerLeak */
+  TLCG_INV_HORIZON_CORRECTNESS = 2, /* CompactionHorizonCorrectness */
+  TLCG_INV_DUP_NULLKEY_MESSAGE = 3  /* DuplicateNullKeyMessage */
+};
+
+/* Next disjuncts, source order (compaction.tla:216-231); -1 = Init */
+enum {
+  TLCG_ACT_INIT = -1,
+  TLCG_ACT_PRODUCER = 0,
+  TLCG_ACT_PHASE_ONE,
+  TLCG_ACT_PHASE_TWO_WRITE,
+  TLCG_ACT_PHASE_TWO_UPDATE_CONTEXT,
+  TLCG_ACT_PHASE_TWO_UPDATE_HORIZON,
+  TLCG_ACT_PHASE_TWO_PERSIST_CURSOR,
+  TLCG_ACT_PHASE_TWO_DELETE_LEDGER,
+  TLCG_ACT_BROKER_CRASH,
+  TLCG_ACT_CONSUMER,
+  TLCG_ACT_TERMINATING
+};
+
+/* run status */
+enum {
+  TLCG_RUNNING = 0,
+  TLCG_DONE = 1,             /* "Model checking completed. No error has been found." */
+  TLCG_VIOLATION = 2,        /* "Invariant X is violated." */
+  TLCG_DEADLOCK = 3,         /* "Deadlock reached." */
+  TLCG_ACTION_ERROR = 4,     /* evaluation error while computing a successor */
+  TLCG_INVARIANT_ERROR = 5   /* evaluation error while evaluating an invariant */
+};
+
+/* The constants of compaction.tla:10-18 as bound by a TLC cfg
+ * (compaction.cfg:2-11), plus the INVARIANTS list (compaction.cfg:25-31). */
+typedef struct tlcg_model {
+  int32_t msg_sent_limit;          /* MessageSentLimit */
+  int32_t compaction_times_limit;  /* CompactionTimesLimit */
+  int32_t consume_times_limit;     /* ConsumeTimesLimit */
+  int32_t max_crash_times;         /* MaxCrashTimes */
+  uint8_t model_consumer;          /* ModelConsumer */
+  uint8_t model_producer;          /* ModelProducer */
+  uint8_t retain_null_key;         /* RetainNullKey */
+  uint8_t check_deadlock;          /* 1 unless TLC's -deadlock flag */
+  int32_t n_keys, n_values;        /* |KeySpace|, |ValueSpace| */
+  int64_t keys[TLCG_MAX_SET];      /* KeySpace elements (any order; 0 is reserved) */
+  int64_t values[TLCG_MAX_SET];    /* ValueSpace elements */
+  int32_t n_invariants;
+  int32_t invariants[TLCG_MAX_INV]; /* TLCG_INV_* in cfg order */
+} tlcg_model;
+
+typedef struct tlcg_opts {
+  int32_t device;            /* HIP device ordinal */
+  int32_t log2_fpset_slots;  /* FPSet size (8-byte slots); 0 = auto, grows on demand */
+  uint64_t state_capacity;   /* states kept for traces; 0 = auto, grows on demand */
+  int32_t tlc_order;         /* 1: order every level like TLC -workers 1 (exact TLC trace) */
+  int32_t rank, world;       /* fingerprint partition: this context owns rank of world */
+  int32_t partition;         /* 0 auto (by `messages` when it is immutable), 1 by `messages`, 2 whole state */
+  int32_t reserved[7];
+} tlcg_opts;
+
+typedef struct tlcg_stats {
+  uint64_t generated;        /* "states generated" (initial states included) */
+  uint64_t distinct;         /* "distinct states found" (this rank) */
+  uint64_t frontier;         /* states of the newest level ("left on queue" when stopped) */
+  int32_t depth;             /* BFS levels so far, the initial level counting as 1 */
+  int32_t status;            /* TLCG_* status */
+  int32_t invariant;         /* index into tlcg_model.invariants of the failing one, else -1 */
+  int32_t action;            /* TLCG_ACT_* of the failing step (or -1) */
+  uint64_t event_gidx;       /* state index of the violating/deadlocked state, or of the
+                                parent of a failing action */
+  double fp_collision_optimistic; /* TLC's estimate d*(g-d)/2^64 (the set itself is exact) */
+  double kernel_ms;          /* total device time of the BFS kernels so far (HIP events) */
+  double expand_ms;          /* device time of the expand kernels alone */
+  uint64_t levels_redone;    /* levels re-run after an FPSet / store growth */
+  uint64_t reserved[4];
+} tlcg_stats;
+
+typedef struct tlcg_ctx tlcg_ctx;
+
+int tlcg_abi_version(void);
+/* ASSUME (compaction.tla:25-35) + packing check.  0 ok, <0 with a message in err. */
+int tlcg_check_model(const tlcg_model* m, char* err, int32_t cap);
+/* bits of the packed state word for these constants (<= 63 supported) */
+int tlcg_state_bits(const tlcg_model* m);
+/* number of initial states (Init, compaction.tla:188-202) */
+uint64_t tlcg_init_count(const tlcg_model* m);
+
+int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out);
+void tlcg_destroy(tlcg_ctx* c);
+const char* tlcg_last_error(const tlcg_ctx* c);
+
+/* (Re)starts a run: clears the FPSet and the queue, then Init. */
+int tlcg_init(tlcg_ctx* c, tlcg_stats* st);
+/* One BFS level (world == 1): expand, dedup, check, enqueue. */
+int tlcg_step_level(tlcg_ctx* c, tlcg_stats* st);
+/* tlcg_init + tlcg_step_level until status != TLCG_RUNNING (world == 1). */
+int tlcg_run(tlcg_ctx* c, tlcg_stats* st);
+
+/* Per-level distinct counts of this rank, level 0 = initial states. */
+int tlcg_level_sizes(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n);
+/* Trace to the event state: states[0] is initial; actions[i] is the step that
+ * produced states[i] (TLCG_ACT_INIT for i = 0).  world == 1 only. */
+int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len);
+/* One stored state and its parent reference ((rank << 56) | parent_gidx << ord_bits | ordinal,
+ * or ~0 for an initial state). */
+int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref);
+/* Copy stored states [first, first + n) to host memory. */
+int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out);
+/* Successor ordinal bits (to split a parent_ref). */
+int tlcg_ordinal_bits(const tlcg_model* m);
+int tlcg_action_of_ordinal(const tlcg_model* m, int32_t ordinal);
+
+/* TLC value syntax of a packed state, "/\ var = value" lines in declaration
+ * order (compaction.tla:57-70).  Host only.  Returns length or <0. */
+int tlcg_decode(const tlcg_model* m, uint64_t state, char* buf, int32_t cap);
+/* Host-side reference semantics of the packed encoding (same code the
+ * kernels run): initial state idx, and the successors of a state in Next
+ * order.  Returns the successor count, or <0 on an evaluation error. */
+uint64_t tlcg_host_init_state(const tlcg_model* m, uint64_t idx);
+int tlcg_host_successors(const tlcg_model* m, uint64_t state, uint64_t* out, int32_t* actions, int32_t cap);
+/* First failing invariant of a state: -1 all hold, else (index << 1) | is_error. */
+int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state);
+/* Owner rank of a state under the context's partition. */
+int tlcg_owner(tlcg_ctx* c, uint64_t state);
+
+/* ---- partitioned (multi-rank) level, world > 1 ----
+ * tlcg_init, then per level: tlcg_expand -> exchange outboxes (e.g. RCCL
+ * all-to-all) -> tlcg_inbox + copy -> tlcg_absorb -> tlcg_end_level.
+ * Records are 16 bytes: {uint64 state, uint64 parent_ref}. */
+int tlcg_expand(tlcg_ctx* c, tlcg_stats* st);
+int tlcg_outbox(tlcg_ctx* c, int32_t dst, void** dev_records, uint64_t* n_records);
+int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records);
+int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st);
+int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st);
+
+/* HIP stream (hipStream_t) the context launches on, for event timing. */
+void* tlcg_stream(tlcg_ctx* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TLCGPU_H */

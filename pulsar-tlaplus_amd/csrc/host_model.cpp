@@ -1,0 +1,315 @@
+// pulsar-tlaplus_amd/csrc/host_model.cpp -- host-only model plumbing and the
+// model-level (context-free) C-ABI entry points.
+#include "host_model.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+namespace tlcg {
+
+static const char* kPhaseName[6] = {
+    "Compactor_In_PhaseOne", "Compactor_In_PhaseTwoWrite", "Compactor_In_PhaseTwoUpdateContext",
+    "Compactor_In_PhaseTwoUpdateHorizon", "Compactor_In_PhaseTwoPersistCusror",
+    "Compactor_In_PhaseTwoDeleteLedger"};
+
+bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
+  // ASSUME, compaction.tla:25-35 (the booleans are typed by the C struct)
+  auto fail = [&](const std::string& s) {
+    if (err) *err = s;
+    return false;
+  };
+  if (m.msg_sent_limit < 0) return fail("Assumption MessageSentLimit \\in Nat is false.");
+  if (m.compaction_times_limit < 0) return fail("Assumption CompactionTimesLimit \\in Nat is false.");
+  if (m.consume_times_limit < 0) return fail("Assumption ConsumeTimesLimit \\in Nat is false.");
+  if (m.max_crash_times < 0) return fail("Assumption MaxCrashTimes \\in Nat is false.");
+  if (m.n_keys < 0 || m.n_keys > TLCG_MAX_SET || m.n_values < 0 || m.n_values > TLCG_MAX_SET)
+    return fail("KeySpace/ValueSpace larger than this build supports (63 elements).");
+  std::vector<int64_t> ks(m.keys, m.keys + m.n_keys), vs(m.values, m.values + m.n_values);
+  for (int64_t k : ks) {
+    if (k < 0) return fail("Assumption KeySpace \\in SUBSET Nat is false.");
+    if (k == 0) return fail("Assumption 0 \\notin KeySpace is false.");
+  }
+  for (int64_t v : vs) {
+    if (v < 0) return fail("Assumption ValueSpace \\in SUBSET Nat is false.");
+    if (v == 0) return fail("Assumption 0 \\notin ValueSpace is false.");
+  }
+  if (m.n_invariants < 0 || m.n_invariants > TLCG_MAX_INV) return fail("too many invariants");
+  for (int q = 0; q < m.n_invariants; ++q)
+    if (m.invariants[q] < 0 || m.invariants[q] >= N_INVARIANT_KINDS) return fail("unknown invariant id");
+  HostModel hm;
+  ks.push_back(0);
+  vs.push_back(0);
+  std::sort(ks.begin(), ks.end());
+  ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+  std::sort(vs.begin(), vs.end());
+  vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
+  hm.keyset = ks;
+  hm.valueset = vs;
+  Layout& L = hm.L;
+  std::memset(&L, 0, sizeof L);
+  L.N = m.msg_sent_limit;
+  L.C = m.compaction_times_limit;
+  L.K = m.max_crash_times;
+  L.ctl = m.consume_times_limit;
+  if (L.N > 32) return fail("MessageSentLimit > 32 is not supported by this build.");
+  if (L.C > 32) return fail("CompactionTimesLimit > 32 is not supported by this build.");
+  L.nk = (int)ks.size();
+  L.nv = (int)vs.size();
+  L.nkv = L.nk * L.nv;
+  L.kb = bits_for((u64)(L.nk - 1));
+  L.vb = bits_for((u64)(L.nv - 1));
+  L.mw = L.kb + L.vb;
+  int sh = 0;
+  L.len_sh = sh; L.len_w = bits_for((u64)L.N); sh += L.len_w;
+  L.msg_sh = sh; sh += L.N * L.mw;
+  L.led_sh = sh; L.led_w = 1 + L.N; sh += L.C * L.led_w;
+  L.p1r_sh = sh; L.p1r_w = bits_for((u64)L.N); sh += L.p1r_w;
+  L.cur_sh = sh; L.curh_w = bits_for((u64)L.N); L.curc_w = bits_for((u64)L.C); sh += 1 + L.curh_w + L.curc_w;
+  L.ph_sh = sh; sh += 3;
+  L.hz_sh = sh; L.hz_w = bits_for((u64)L.N); sh += L.hz_w;
+  L.ctx_sh = sh; L.ctx_w = bits_for((u64)L.C); sh += L.ctx_w;
+  L.cr_sh = sh; L.cr_w = bits_for((u64)L.K); sh += L.cr_w;
+  L.bits = sh;
+  if (L.bits > 63) {
+    char b[160];
+    std::snprintf(b, sizeof b, "these constants need a %d-bit state; this build packs states into 63 bits", L.bits);
+    return fail(b);
+  }
+  L.retain = m.retain_null_key ? 1 : 0;
+  L.producer = m.model_producer ? 1 : 0;
+  L.consumer = m.model_consumer ? 1 : 0;
+  // Terminating's last conjunct: ModelConsumer => consumeTimes = ConsumeTimesLimit,
+  // with consumeTimes constantly 0.
+  L.term_ok = (!L.consumer || L.ctl == 0) ? 1 : 0;
+  L.check_deadlock = m.check_deadlock ? 1 : 0;
+  L.ord_bits = bits_for((u64)(L.nkv + N_ACTIONS - 1));
+  L.n_inv = m.n_invariants;
+  for (int q = 0; q < m.n_invariants; ++q) L.inv[q] = m.invariants[q];
+  L.msgs_mask = (L.msg_sh + L.N * L.mw) >= 64 ? ~0ull : ((1ull << (L.msg_sh + L.N * L.mw)) - 1);
+  L.led_present_mask = 0;
+  for (int j = 1; j <= L.C; ++j) L.led_present_mask |= 1ull << led_base(L, j);
+  // initial states
+  if (L.producer) {
+    hm.n_init = 1;
+  } else {
+    long double n = 1;
+    for (int i = 0; i < L.N; ++i) n *= (long double)L.nkv;
+    if (n > (long double)(1ull << 40)) return fail("more than 2^40 initial states");
+    u64 c = 1;
+    for (int i = 0; i < L.N; ++i) c *= (u64)L.nkv;
+    hm.n_init = c;
+  }
+  hm.max_new_per_state = (L.producer ? L.nkv : 0) + 2;
+  *out = hm;
+  return true;
+}
+
+std::string format_state(const HostModel& hm, u64 s) {
+  const Layout& L = hm.L;
+  std::ostringstream o;
+  int len = st_len(L, s);
+  auto msg = [&](int p) {
+    o << "[id |-> " << p << ", key |-> " << hm.keyset[st_key(L, s, p)] << ", value |-> "
+      << hm.valueset[st_val(L, s, p)] << "]";
+  };
+  o << "/\\ messages = <<";
+  for (int p = 1; p <= len; ++p) {
+    if (p > 1) o << ", ";
+    msg(p);
+  }
+  o << ">>\n/\\ compactedLedgers = <<";
+  for (int j = 1; j <= L.C; ++j) {
+    if (j > 1) o << ", ";
+    if (!led_present(L, s, j)) {
+      o << "Nil";
+      continue;
+    }
+    u64 mk = led_mask(L, s, j);
+    o << "<<";
+    bool first = true;
+    for (int p = 1; p <= L.N; ++p)
+      if ((mk >> (p - 1)) & 1) {
+        if (!first) o << ", ";
+        msg(p);
+        first = false;
+      }
+    o << ">>";
+  }
+  o << ">>\n/\\ cursor = ";
+  if (!cur_present(L, s)) o << "Nil";
+  else o << "[compactedTopicContext |-> " << cur_c(L, s) << ", compactionHorizon |-> " << cur_h(L, s) << "]";
+  o << "\n/\\ compactorState = " << kPhaseName[st_phase(L, s) < 6 ? st_phase(L, s) : 0];
+  o << "\n/\\ phaseOneResult = ";
+  int r = st_p1r(L, s);
+  if (r == 0) {
+    o << "Nil";
+  } else {
+    // latestForKey == [key \in GetKeys(messages[1..r]) |-> Max(...)] (compaction.tla:97-98)
+    std::vector<std::pair<int64_t, int>> f;
+    for (int ki = 1; ki < L.nk; ++ki) {
+      int mx = 0;
+      for (int p = 1; p <= r; ++p)
+        if (st_key(L, s, p) == ki) mx = p;
+      if (mx) f.push_back({hm.keyset[ki], mx});
+    }
+    bool tuple = true;
+    for (size_t i = 0; i < f.size(); ++i)
+      if (f[i].first != (int64_t)(i + 1)) tuple = false;
+    o << "[latestForKey |-> ";
+    if (tuple) {
+      o << "<<";
+      for (size_t i = 0; i < f.size(); ++i) o << (i ? ", " : "") << f[i].second;
+      o << ">>";
+    } else {
+      o << "(";
+      for (size_t i = 0; i < f.size(); ++i) o << (i ? " @@ " : "") << f[i].first << " :> " << f[i].second;
+      o << ")";
+    }
+    o << ", readPosition |-> " << r << "]";
+  }
+  o << "\n/\\ compactionHorizon = " << st_hz(L, s);
+  o << "\n/\\ compactedTopicContext = " << st_ctx(L, s);
+  o << "\n/\\ crashTimes = " << st_crash(L, s);
+  o << "\n/\\ consumeTimes = 0";
+  return o.str();
+}
+
+int successor_at(const Layout& L, u64 s, int ord, u64* t) {
+  int act = action_of_ordinal(L, ord);
+  if (act == ACT_PRODUCER) {
+    if (!L.producer) return 0;
+    int len = st_len(L, s);
+    if (len >= L.N) return 0;
+    *t = producer_succ(L, s, len, ord);
+    return 1;
+  }
+  if (act == ACT_CRASH) return crash_step(L, s, t);
+  if (act == ACT_CONSUMER) {
+    if (!L.consumer) return 0;
+    *t = s;
+    return 1;
+  }
+  if (act == ACT_TERMINATING) {
+    if (!terminating_enabled(L, s)) return 0;
+    *t = s;
+    return 1;
+  }
+  int a2 = -1;
+  u64 u = 0;
+  int r = compactor_step(L, s, &u, &a2);
+  if (r == 0 || a2 != act) return 0;
+  if (r == 2) return 2;
+  *t = u;
+  return 1;
+}
+
+int host_successors(const Layout& L, u64 s, u64* out, int* actions, int cap) {
+  int n = 0;
+  auto put = [&](u64 t, int a) {
+    if (n < cap) {
+      out[n] = t;
+      if (actions) actions[n] = a;
+    }
+    ++n;
+  };
+  if (L.producer) {
+    int len = st_len(L, s);
+    if (len < L.N)
+      for (int j = 0; j < L.nkv; ++j) put(producer_succ(L, s, len, j), ACT_PRODUCER);
+  }
+  u64 t;
+  int act;
+  int r = compactor_step(L, s, &t, &act);
+  if (r == 2) return -1;
+  if (r == 1) put(t, act);
+  if (crash_step(L, s, &t)) put(t, ACT_CRASH);
+  if (L.consumer) put(s, ACT_CONSUMER);
+  if (terminating_enabled(L, s)) put(s, ACT_TERMINATING);
+  return n;
+}
+
+}  // namespace tlcg
+
+using namespace tlcg;
+
+extern "C" {
+
+int tlcg_abi_version(void) { return TLCG_ABI_VERSION; }
+
+int tlcg_check_model(const tlcg_model* m, char* err, int32_t cap) {
+  HostModel hm;
+  std::string e;
+  if (!m) return -1;
+  if (!build_model(*m, &hm, &e)) {
+    if (err && cap > 0) std::snprintf(err, (size_t)cap, "%s", e.c_str());
+    return -1;
+  }
+  if (err && cap > 0) err[0] = 0;
+  return 0;
+}
+
+int tlcg_state_bits(const tlcg_model* m) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -1;
+  return hm.L.bits;
+}
+
+uint64_t tlcg_init_count(const tlcg_model* m) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return 0;
+  return hm.n_init;
+}
+
+int tlcg_ordinal_bits(const tlcg_model* m) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -1;
+  return hm.L.ord_bits;
+}
+
+int tlcg_action_of_ordinal(const tlcg_model* m, int32_t ordinal) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -2;
+  return action_of_ordinal(hm.L, ordinal);
+}
+
+int tlcg_decode(const tlcg_model* m, uint64_t state, char* buf, int32_t cap) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -1;
+  std::string s = format_state(hm, state);
+  if (buf && cap > 0) std::snprintf(buf, (size_t)cap, "%s", s.c_str());
+  return (int)s.size();
+}
+
+uint64_t tlcg_host_init_state(const tlcg_model* m, uint64_t idx) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return ~0ull;
+  return init_state(hm.L, idx);
+}
+
+int tlcg_host_successors(const tlcg_model* m, uint64_t state, uint64_t* out, int32_t* actions, int32_t cap) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -2;
+  std::vector<int> acts((size_t)std::max(cap, 0));
+  int n = host_successors(hm.L, state, out, acts.data(), cap);
+  if (actions)
+    for (int i = 0; i < std::min(n, (int)cap); ++i) actions[i] = acts[(size_t)i];
+  return n;
+}
+
+int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -2;
+  return check_invariants(hm.L, state);
+}
+
+}  // extern "C"

@@ -1,0 +1,1053 @@
+// pulsar-tlaplus_amd/csrc/tlcgpu.hip -- the gfx950 BFS level kernels and the
+// host runtime behind include/tlcgpu.h.
+//
+// One BFS level = one `k_expand` launch over the frontier (a contiguous slice
+// of the resident state store).  Per parent state the kernel evaluates the
+// Next disjuncts (compaction.tla:216-231) on the packed word, counts every
+// successor as generated, inserts non-stuttering successors into the HBM
+// FPSet with a 64-bit CAS, checks invariants on the new ones, and appends them
+// (wave ballot -> LDS stage -> one global atomic per block chunk) to the next
+// level together with a parent-pointer entry for traces.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "host_model.h"
+#include "kernels.h"
+#include "tlcgpu.h"
+
+using namespace tlcg;
+
+namespace {
+
+struct ExpandArgs {
+  Layout L;
+  const u64* frontier;
+  u64 n_front;
+  u64 front_gidx0;  // gidx of frontier[0]
+  u64* slots;
+  int log2;
+  u64* states_out;  // next level (store + level_base[d+1])
+  u64* parents_out;
+  u64 cap_out;      // room for new states
+  u64* slot_out;    // TLC order: FPSet slot of every new state
+  u64* dkey_slot;   // TLC order: min discovery key per FPSet slot
+  LevelCtr* ctr;
+  u64 rank_tag;     // rank << 56
+  int rank, world;
+  u64 owner_mask;
+  u64* outbox;      // world > 1: [world][outbox_cap] records {state, parent_ref}
+  u64 outbox_cap;
+};
+
+__device__ __forceinline__ int owner_of(u64 s, u64 owner_mask, int world) {
+  return (int)(((mix64(s & owner_mask) >> 32) * (u64)world) >> 32);
+}
+
+// ---- Init (compaction.tla:188-202), world == 1: initial state idx goes to
+// store position idx, which is also TLC's enumeration order.
+__global__ __launch_bounds__(BLOCK) void k_init_direct(Layout L, u64 n_init, u64* __restrict__ slots, int log2,
+                                                       u64* __restrict__ states, u64* __restrict__ parents,
+                                                       LevelCtr* ctr) {
+  const u64 idx = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (idx >= n_init) return;
+  const u64 s = init_state(L, idx);
+  u64 slot;
+  const int r = fpset_put(slots, log2, s, mix64(s), &slot);
+  if (r < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+  if (r == 0) atomicOr(&ctr->overflow, (unsigned)OVF_DUP_INIT);
+  states[idx] = s;
+  parents[idx] = NO_PARENT;
+  const int c = check_invariants(L, s);
+  if (c >= 0) atomicMin(&ctr->event, make_event(idx, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+}
+
+// ---- Init, world > 1: keep only the initial states this rank owns.
+__global__ __launch_bounds__(BLOCK) void k_init_part(Layout L, u64 n_init, int rank, int world, u64 owner_mask,
+                                                     u64* __restrict__ slots, int log2, u64* __restrict__ states,
+                                                     u64* __restrict__ parents, u64 cap, LevelCtr* ctr) {
+  __shared__ u64 s_st[BLOCK], s_par[BLOCK];
+  __shared__ unsigned s_cnt;
+  __shared__ unsigned long long s_base;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const u64 idx = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  bool mine = false;
+  u64 s = 0;
+  if (idx < n_init) {
+    s = init_state(L, idx);
+    if (owner_of(s, owner_mask, world) == rank) {
+      u64 slot;
+      const int r = fpset_put(slots, log2, s, mix64(s), &slot);
+      if (r < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+      mine = r == 1;
+      if (mine) {
+        const int c = check_invariants(L, s);
+        if (c >= 0) atomicMin(&ctr->event, make_event(idx, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+      }
+    }
+  }
+  stage_append<false>(mine, s, NO_PARENT, 0, s_st, s_par, nullptr, &s_cnt);
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&ctr->n_new, (unsigned long long)s_cnt) : 0;
+  __syncthreads();
+  const unsigned n = s_cnt;
+  const u64 b = s_base;
+  if (b + n > cap) {
+    if (threadIdx.x == 0) atomicOr(&ctr->overflow, (unsigned)OVF_STORE);
+    return;
+  }
+  for (unsigned i = threadIdx.x; i < n; i += BLOCK) {
+    states[b + i] = s_st[i];
+    parents[b + i] = s_par[i];
+  }
+}
+
+// ---- one BFS level ----
+template <bool PRODUCER, bool TLC, bool PART>
+__global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
+  __shared__ u64 s_st[STAGE_CAP];
+  __shared__ u64 s_par[STAGE_CAP];
+  __shared__ u64 s_slot[TLC ? STAGE_CAP : 1];
+  __shared__ unsigned s_cnt;
+  __shared__ unsigned long long s_base;
+  const Layout& L = a.L;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  u64 gen = 0;
+  unsigned long long ev = NO_EVENT;
+
+  // emit one successor (all lanes of the wave call this)
+  auto emit = [&](bool pred, u64 t, u64 dkey) {
+    bool isnew = false;
+    u64 slot = 0;
+    if (pred) {
+      bool local = true;
+      if (PART) {
+        const int dst = owner_of(t, a.owner_mask, a.world);
+        if (dst != a.rank) {
+          local = false;
+          const unsigned long long pos = atomicAdd(&a.ctr->n_out[dst], 1ull);
+          if (pos < a.outbox_cap) {
+            u64* rec = a.outbox + 2 * ((u64)dst * a.outbox_cap + pos);
+            rec[0] = t;
+            rec[1] = a.rank_tag | dkey;
+          } else {
+            atomicOr(&a.ctr->overflow, (unsigned)OVF_OUTBOX);
+          }
+        }
+      }
+      if (local) {
+        const int r = fpset_put(a.slots, a.log2, t, mix64(t), &slot);
+        if (r < 0) atomicOr(&a.ctr->overflow, (unsigned)OVF_FPSET);
+        isnew = r == 1;
+        if (TLC && r >= 0) atomicMin((unsigned long long*)&a.dkey_slot[slot], (unsigned long long)dkey);
+        if (!TLC && isnew) {
+          const int c = check_invariants(L, t);
+          if (c >= 0) ev = min(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+        }
+      }
+    }
+    stage_append<TLC>(isnew, t, a.rank_tag | dkey, slot, s_st, s_par, s_slot, &s_cnt);
+  };
+
+  auto flush = [&]() {
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&a.ctr->n_new, (unsigned long long)s_cnt) : 0;
+    __syncthreads();
+    const unsigned n = s_cnt;
+    const u64 b = s_base;
+    if (b + n <= a.cap_out) {
+      for (unsigned i = threadIdx.x; i < n; i += BLOCK) {
+        a.states_out[b + i] = s_st[i];
+        a.parents_out[b + i] = s_par[i];
+        if (TLC) a.slot_out[b + i] = s_slot[i];
+      }
+    } else if (threadIdx.x == 0 && n) {
+      atomicOr(&a.ctr->overflow, (unsigned)OVF_STORE);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  };
+
+  // room check at a block-uniform point: flush if `upcoming` more emits could overflow the stage
+  auto reserve = [&](int upcoming) {
+    __syncthreads();
+    const unsigned n = s_cnt;
+    __syncthreads();
+    if (n + (unsigned)upcoming * BLOCK > (unsigned)STAGE_CAP) flush();
+  };
+
+  constexpr int kItems = PRODUCER ? 1 : ITEMS;
+  const u64 per_chunk = (u64)BLOCK * kItems;
+  const u64 ord_last = (1ull << L.ord_bits) - 1;
+  for (u64 c0 = (u64)blockIdx.x * per_chunk; c0 < a.n_front; c0 += (u64)gridDim.x * per_chunk) {
+#pragma unroll 1
+    for (int it = 0; it < kItems; ++it) {
+      const u64 pi = c0 + (u64)it * BLOCK + threadIdx.x;
+      const bool valid = pi < a.n_front;
+      const u64 s = valid ? a.frontier[pi] : 0;
+      const u64 dk0 = (a.front_gidx0 + pi) << L.ord_bits;
+      int nsucc = 0;
+      if (PRODUCER) {  // Producer, compaction.tla:83-87
+        const int len = st_len(L, s);
+        const bool can = valid && len < L.N;
+#pragma unroll 1
+        for (int j = 0; j < L.nkv; ++j) {
+          if ((j & 3) == 0) reserve(6);
+          emit(can, can ? producer_succ(L, s, len, j) : 0, dk0 | (u64)j);
+        }
+        nsucc += can ? L.nkv : 0;
+        reserve(2);
+      }
+      // the compactor disjuncts, compaction.tla:221-226
+      u64 t = 0;
+      int act = 0;
+      const int r = valid ? compactor_step(L, s, &t, &act) : 0;
+      if (r == 2) ev = min(ev, (unsigned long long)make_event(dk0 | (u64)ordinal_of(L, act, 0), EVK_ACTION_ERROR, act));
+      nsucc += (r == 1);
+      emit(r == 1, t, dk0 | (u64)ordinal_of(L, act, 0));
+      // BrokerCrash, compaction.tla:227
+      u64 t2 = 0;
+      const bool en2 = valid && crash_step(L, s, &t2);
+      nsucc += en2;
+      emit(en2, t2, dk0 | (u64)ordinal_of(L, ACT_CRASH, 0));
+      // Consumer / Terminating: stuttering successors, generated but never new
+      if (valid) nsucc += selfloop_count(L, s);
+      gen += (u64)nsucc;
+      if (valid && nsucc == 0 && L.check_deadlock)
+        ev = min(ev, (unsigned long long)make_event(dk0 | ord_last, EVK_DEADLOCK, 0));
+    }
+    flush();
+  }
+  gen = wave_sum_u64(gen);
+  if (__lane_id() == 0 && gen) atomicAdd(&a.ctr->generated, (unsigned long long)gen);
+  if (ev != NO_EVENT) atomicMin(&a.ctr->event, ev);
+}
+
+// ---- TLC order: gather each new state's minimal discovery key
+__global__ __launch_bounds__(BLOCK) void k_gather_dkey(u64 n, const u64* __restrict__ slot_new,
+                                                       const u64* __restrict__ dkey_slot, u64* __restrict__ dk) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (i < n) dk[i] = dkey_slot[slot_new[i]];
+}
+
+// ---- TLC order: write the level back in discovery order, parent = first
+// discoverer, invariants on each new state keyed by its discovery key.
+__global__ __launch_bounds__(BLOCK) void k_tlc_finish(Layout L, u64 n, const u64* __restrict__ st_sorted,
+                                                      const u64* __restrict__ dk_sorted, u64* __restrict__ states,
+                                                      u64* __restrict__ parents, u64 rank_tag, LevelCtr* ctr) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const u64 s = st_sorted[i], dk = dk_sorted[i];
+  states[i] = s;
+  parents[i] = rank_tag | dk;
+  const int c = check_invariants(L, s);
+  if (c >= 0) atomicMin(&ctr->event, make_event(dk, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+}
+
+// ---- FPSet growth: re-insert every stored state
+__global__ __launch_bounds__(BLOCK) void k_reinsert(const u64* __restrict__ states, u64 n, u64* __restrict__ slots,
+                                                    int log2, LevelCtr* ctr) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const u64 s = states[i];
+  u64 slot;
+  if (fpset_put(slots, log2, s, mix64(s), &slot) < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+}
+
+// ---- world > 1: insert successors received from other ranks
+__global__ __launch_bounds__(BLOCK) void k_absorb(Layout L, const u64* __restrict__ recs, u64 n,
+                                                  u64* __restrict__ slots, int log2, u64* __restrict__ states_out,
+                                                  u64* __restrict__ parents_out, u64 cap, LevelCtr* ctr) {
+  __shared__ u64 s_st[BLOCK], s_par[BLOCK];
+  __shared__ unsigned s_cnt;
+  __shared__ unsigned long long s_base;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  bool isnew = false;
+  u64 t = 0, ref = 0;
+  if (i < n) {
+    t = recs[2 * i];
+    ref = recs[2 * i + 1];
+    u64 slot;
+    const int r = fpset_put(slots, log2, t, mix64(t), &slot);
+    if (r < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+    isnew = r == 1;
+    if (isnew) {
+      const int c = check_invariants(L, t);
+      // keyed by inbox position, tagged with bit 57 (resolved on the host)
+      if (c >= 0)
+        atomicMin(&ctr->event, make_event((1ull << 51) | i, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+    }
+  }
+  stage_append<false>(isnew, t, ref, 0, s_st, s_par, nullptr, &s_cnt);
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&ctr->n_new, (unsigned long long)s_cnt) : 0;
+  __syncthreads();
+  const unsigned m = s_cnt;
+  const u64 b = s_base;
+  if (b + m > cap) {
+    if (threadIdx.x == 0) atomicOr(&ctr->overflow, (unsigned)OVF_STORE);
+    return;
+  }
+  for (unsigned k = threadIdx.x; k < m; k += BLOCK) {
+    states_out[b + k] = s_st[k];
+    parents_out[b + k] = s_par[k];
+  }
+}
+
+inline unsigned grid_for(u64 n, u64 per_block, unsigned cap) {
+  u64 g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (unsigned)std::min<u64>(g, cap);
+}
+
+}  // namespace
+
+// ======================= host runtime =======================
+
+struct tlcg_ctx {
+  tlcg_model model;
+  tlcg_opts opts;
+  HostModel hm;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+  // FPSet
+  u64* d_slots = nullptr;
+  int log2 = 0;
+  u64* d_dkey_slot = nullptr;  // TLC order
+  // state store (all levels) + parent log
+  u64* d_states = nullptr;
+  u64* d_parents = nullptr;
+  u64 cap = 0;
+  // TLC-order scratch
+  u64* d_slot_new = nullptr;
+  u64* d_dk = nullptr;
+  u64* d_dk2 = nullptr;
+  u64* d_st2 = nullptr;
+  void* d_sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
+  u64 scratch_cap = 0;
+  // partition exchange
+  u64* d_outbox = nullptr;
+  u64 outbox_cap = 0;  // records per destination
+  u64* d_inbox = nullptr;
+  u64 inbox_cap = 0;
+  u64 absorbed_new = 0;
+  // counters
+  LevelCtr* d_ctr = nullptr;
+  LevelCtr* h_ctr = nullptr;
+  // run state
+  std::vector<u64> level_base;  // level_base[d] = gidx of the first state of level d
+  u64 generated = 0;
+  int status = TLCG_RUNNING;
+  u64 ev_word = NO_EVENT;
+  int ev_level = -1;  // level whose expansion raised the event (0 = Init)
+  u64 ev_state = 0;
+  u64 ev_parent_gidx = NO_PARENT;
+  u64 ev_parent_ref = NO_PARENT;
+  int ev_action = -1;
+  double kernel_ms = 0, expand_ms = 0;
+  u64 levels_redone = 0;
+  u64 owner_mask = ~0ull;
+  std::string err;
+  bool inited = false;
+};
+
+namespace {
+
+#define HIPCHK(expr)                                                              \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      c->err = std::string(#expr) + ": " + hipGetErrorString(_e);                 \
+      return false;                                                               \
+    }                                                                             \
+  } while (0)
+
+u64 distinct_of(const tlcg_ctx* c) { return c->level_base.empty() ? 0 : c->level_base.back(); }
+
+bool alloc_bytes(tlcg_ctx* c, void** p, size_t bytes, const char* what) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    char b[256];
+    std::snprintf(b, sizeof b, "out of device memory allocating %s (%.2f GiB): %s", what,
+                  bytes / 1073741824.0, hipGetErrorString(e));
+    c->err = b;
+    *p = nullptr;
+    return false;
+  }
+  return true;
+}
+
+// grow the state store so that it holds `need` states (keeps contents)
+bool ensure_store(tlcg_ctx* c, u64 need) {
+  if (need <= c->cap) return true;
+  u64 ncap = std::max<u64>(need + need / 4, c->cap * 2);
+  ncap = std::max<u64>(ncap, 1u << 16);
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+    u64 room = (u64)(fr * 0.9) / 16 + c->cap;  // both arrays; old ones freed after copy
+    if (ncap > room && need <= room) ncap = room;
+  }
+  u64 *ns = nullptr, *np = nullptr;
+  if (!alloc_bytes(c, (void**)&ns, ncap * 8, "state store")) return false;
+  if (!alloc_bytes(c, (void**)&np, ncap * 8, "parent log")) { hipFree(ns); return false; }
+  const u64 keep = distinct_of(c);
+  if (keep) {
+    HIPCHK(hipMemcpyAsync(ns, c->d_states, keep * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(np, c->d_parents, keep * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  hipFree(c->d_states);
+  hipFree(c->d_parents);
+  c->d_states = ns;
+  c->d_parents = np;
+  c->cap = ncap;
+  return true;
+}
+
+// (re)build the FPSet at 2^log2 slots holding states[0, n)
+bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
+  if (log2 != c->log2 || !c->d_slots) {
+    hipFree(c->d_slots);
+    c->d_slots = nullptr;
+    hipFree(c->d_dkey_slot);
+    c->d_dkey_slot = nullptr;
+    if (!alloc_bytes(c, (void**)&c->d_slots, (8ull << log2), "FPSet")) return false;
+    if (c->opts.tlc_order && !alloc_bytes(c, (void**)&c->d_dkey_slot, (8ull << log2), "FPSet discovery keys"))
+      return false;
+    c->log2 = log2;
+  }
+  HIPCHK(hipMemsetAsync(c->d_slots, 0, 8ull << log2, c->stream));
+  if (c->d_dkey_slot) HIPCHK(hipMemsetAsync(c->d_dkey_slot, 0xFF, 8ull << log2, c->stream));
+  if (n) {
+    HIPCHK(hipMemsetAsync(c->d_ctr, 0, sizeof(LevelCtr), c->stream));
+    k_reinsert<<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(c->d_states, n, c->d_slots, log2, c->d_ctr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_ctr, c->d_ctr, sizeof(LevelCtr), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->h_ctr->overflow) {
+      c->err = "FPSet rebuild overflowed";
+      return false;
+    }
+  }
+  return true;
+}
+
+// keep the FPSet load <= 1/2 for `need` states
+bool ensure_fpset(tlcg_ctx* c, u64 need) {
+  int l = std::max(c->log2, 16);
+  while ((1ull << l) < 2 * need && l < 40) ++l;
+  if (c->d_slots && l == c->log2) return true;
+  return rebuild_fpset(c, l, distinct_of(c));
+}
+
+bool ensure_scratch(tlcg_ctx* c, u64 n) {
+  if (!c->opts.tlc_order || n <= c->scratch_cap) return true;
+  u64 ncap = std::max<u64>(n + n / 4, 1u << 16);
+  hipFree(c->d_slot_new); hipFree(c->d_dk); hipFree(c->d_dk2); hipFree(c->d_st2); hipFree(c->d_sort_tmp);
+  c->d_slot_new = c->d_dk = c->d_dk2 = c->d_st2 = nullptr;
+  c->d_sort_tmp = nullptr;
+  c->scratch_cap = 0;
+  if (!alloc_bytes(c, (void**)&c->d_slot_new, ncap * 8, "TLC-order scratch")) return false;
+  if (!alloc_bytes(c, (void**)&c->d_dk, ncap * 8, "TLC-order scratch")) return false;
+  if (!alloc_bytes(c, (void**)&c->d_dk2, ncap * 8, "TLC-order scratch")) return false;
+  if (!alloc_bytes(c, (void**)&c->d_st2, ncap * 8, "TLC-order scratch")) return false;
+  size_t tmp = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const u64*)nullptr, (u64*)nullptr, (const u64*)nullptr,
+                                            (u64*)nullptr, (int)std::min<u64>(ncap, 0x7fffffffull), 0, 64,
+                                            c->stream));
+  if (!alloc_bytes(c, &c->d_sort_tmp, tmp, "sort scratch")) return false;
+  c->sort_tmp_bytes = tmp;
+  c->scratch_cap = ncap;
+  return true;
+}
+
+bool reset_ctr(tlcg_ctx* c) {
+  HIPCHK(hipMemsetAsync(c->d_ctr, 0, sizeof(LevelCtr), c->stream));
+  HIPCHK(hipMemsetAsync(&c->d_ctr->event, 0xFF, sizeof(unsigned long long), c->stream));
+  return true;
+}
+
+bool read_ctr(tlcg_ctx* c) {
+  HIPCHK(hipMemcpyAsync(c->h_ctr, c->d_ctr, sizeof(LevelCtr), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return true;
+}
+
+void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
+  if (!st) return;
+  std::memset(st, 0, sizeof *st);
+  const u64 d = distinct_of(c);
+  const int depth = c->level_base.empty() ? 0 : (int)c->level_base.size() - 1;
+  st->generated = c->generated;
+  st->distinct = d;
+  st->frontier = depth ? c->level_base[(size_t)depth] - c->level_base[(size_t)depth - 1] : 0;
+  st->depth = depth;
+  st->status = c->status;
+  st->invariant = -1;
+  st->action = -1;
+  st->event_gidx = c->ev_parent_gidx;
+  if (c->ev_word != NO_EVENT) {
+    const int kind = (int)((c->ev_word >> 4) & 3);
+    if (kind == EVK_VIOLATION || kind == EVK_INV_ERROR) st->invariant = (int)(c->ev_word & 15);
+    st->action = c->ev_action;
+  }
+  const double g = (double)c->generated, n = (double)d;
+  st->fp_collision_optimistic = n * (g - n) / 18446744073709551616.0;
+  st->kernel_ms = c->kernel_ms;
+  st->expand_ms = c->expand_ms;
+  st->levels_redone = c->levels_redone;
+}
+
+bool state_at(tlcg_ctx* c, u64 g, u64* s, u64* p) {
+  HIPCHK(hipMemcpy(s, c->d_states + g, 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(p, c->d_parents + g, 8, hipMemcpyDeviceToHost));
+  return true;
+}
+
+// Interpret the level's event word (world == 1 or a local event).
+bool resolve_event(tlcg_ctx* c, u64 ev, int level) {
+  const Layout& L = c->hm.L;
+  c->ev_word = ev;
+  c->ev_level = level;
+  const int kind = (int)((ev >> 4) & 3);
+  const int index = (int)(ev & 15);
+  const u64 dkey = ev >> 6;
+  switch (kind) {
+    case EVK_VIOLATION: c->status = TLCG_VIOLATION; break;
+    case EVK_INV_ERROR: c->status = TLCG_INVARIANT_ERROR; break;
+    case EVK_DEADLOCK: c->status = TLCG_DEADLOCK; break;
+    default: c->status = TLCG_ACTION_ERROR; break;
+  }
+  if (level == 0) {  // an initial state (dkey = enumeration index)
+    c->ev_state = init_state(L, dkey);
+    c->ev_parent_gidx = NO_PARENT;
+    c->ev_action = TLCG_ACT_INIT;
+    return true;
+  }
+  if ((dkey >> 51) & 1) {  // a state absorbed from another rank: inbox position
+    const u64 i = dkey & ((1ull << 51) - 1);
+    u64 rec[2];
+    HIPCHK(hipMemcpy(rec, c->d_inbox + 2 * i, 16, hipMemcpyDeviceToHost));
+    c->ev_state = rec[0];
+    c->ev_parent_ref = rec[1];
+    c->ev_parent_gidx = NO_PARENT;
+    c->ev_action = action_of_ordinal(L, (int)(rec[1] & ((1ull << L.ord_bits) - 1)));
+    return true;
+  }
+  const u64 pg = dkey >> L.ord_bits;
+  const int ord = (int)(dkey & ((1ull << L.ord_bits) - 1));
+  u64 ps = 0, pp = 0;
+  if (!state_at(c, pg, &ps, &pp)) return false;
+  c->ev_parent_gidx = pg;
+  c->ev_parent_ref = ((u64)c->opts.rank << 56) | dkey;
+  if (kind == EVK_DEADLOCK) {
+    c->ev_state = ps;
+    c->ev_action = -1;
+  } else if (kind == EVK_ACTION_ERROR) {
+    c->ev_state = ps;
+    c->ev_action = index;
+  } else {
+    u64 t = 0;
+    if (successor_at(L, ps, ord, &t) != 1) {
+      c->err = "internal: violating successor could not be re-derived";
+      return false;
+    }
+    c->ev_state = t;
+    c->ev_action = action_of_ordinal(L, ord);
+  }
+  return true;
+}
+
+bool run_init(tlcg_ctx* c) {
+  const HostModel& hm = c->hm;
+  const Layout& L = hm.L;
+  c->level_base.assign(1, 0);
+  c->generated = 0;
+  c->status = TLCG_RUNNING;
+  c->ev_word = NO_EVENT;
+  c->ev_level = -1;
+  c->ev_parent_gidx = NO_PARENT;
+  c->ev_parent_ref = NO_PARENT;
+  c->ev_action = -1;
+  c->kernel_ms = c->expand_ms = 0;
+  c->levels_redone = 0;
+  const int world = c->opts.world;
+  u64 expect = world == 1 ? hm.n_init : hm.n_init / (u64)world + hm.n_init / (u64)(4 * world) + 4096;
+  expect = std::min(expect, hm.n_init);
+  if (!ensure_store(c, expect)) return false;
+  if (!c->d_slots) {
+    int l = c->opts.log2_fpset_slots > 0 ? c->opts.log2_fpset_slots : 16;
+    while ((1ull << l) < 2 * expect && c->opts.log2_fpset_slots <= 0 && l < 40) ++l;
+    if (!rebuild_fpset(c, l, 0)) return false;
+  } else {
+    if (!rebuild_fpset(c, c->log2, 0)) return false;  // clear
+    if (!ensure_fpset(c, expect)) return false;
+  }
+  for (;;) {
+    if (!reset_ctr(c)) return false;
+    HIPCHK(hipEventRecord(c->e0, c->stream));
+    if (world == 1) {
+      k_init_direct<<<grid_for(hm.n_init, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
+          L, hm.n_init, c->d_slots, c->log2, c->d_states, c->d_parents, c->d_ctr);
+    } else {
+      k_init_part<<<grid_for(hm.n_init, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
+          L, hm.n_init, c->opts.rank, world, c->owner_mask, c->d_slots, c->log2, c->d_states, c->d_parents,
+          c->cap, c->d_ctr);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->e1, c->stream));
+    if (!read_ctr(c)) return false;
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->e0, c->e1);
+    c->kernel_ms += ms;
+    const unsigned ovf = c->h_ctr->overflow;
+    if (ovf & OVF_DUP_INIT) {
+      c->err = "internal: duplicate initial state";
+      return false;
+    }
+    if (!ovf) break;
+    ++c->levels_redone;
+    if (ovf & OVF_STORE) {
+      if (!ensure_store(c, std::max<u64>(c->h_ctr->n_new, c->cap * 2))) return false;
+    }
+    if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), 0)) return false;
+  }
+  const u64 n_new = world == 1 ? hm.n_init : c->h_ctr->n_new;
+  c->generated = n_new;
+  // partitioned ranks keep every level (possibly empty) so that level d is
+  // the same BFS level on every rank; termination is decided globally.
+  if (n_new || world > 1) c->level_base.push_back(n_new);
+  if (c->h_ctr->event != NO_EVENT) return resolve_event(c, c->h_ctr->event, 0);
+  if (!n_new && world == 1) c->status = TLCG_DONE;
+  return true;
+}
+
+template <bool P, bool T, bool X>
+void launch_expand_t(const ExpandArgs& a, unsigned grid, hipStream_t s) {
+  k_expand<P, T, X><<<grid, BLOCK, 0, s>>>(a);
+}
+
+bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
+  const Layout& L = c->hm.L;
+  ExpandArgs a;
+  a.L = L;
+  a.frontier = c->d_states + front0;
+  a.n_front = n_front;
+  a.front_gidx0 = front0;
+  a.slots = c->d_slots;
+  a.log2 = c->log2;
+  const u64 d = distinct_of(c);
+  a.states_out = c->d_states + d;
+  a.parents_out = c->d_parents + d;
+  a.cap_out = c->cap - d;
+  a.slot_out = c->d_slot_new;
+  a.dkey_slot = c->d_dkey_slot;
+  a.ctr = c->d_ctr;
+  a.rank_tag = (u64)c->opts.rank << 56;
+  a.rank = c->opts.rank;
+  a.world = c->opts.world;
+  a.owner_mask = c->owner_mask;
+  a.outbox = c->d_outbox;
+  a.outbox_cap = c->outbox_cap;
+  const bool prod = L.producer != 0, tlc = c->opts.tlc_order != 0;
+  const u64 per_block = (u64)BLOCK * (prod ? 1 : ITEMS);
+  const unsigned grid = grid_for(n_front, per_block, 8192);
+  if (prod) {
+    if (tlc) launch_expand_t<true, true, false>(a, grid, c->stream);
+    else if (part) launch_expand_t<true, false, true>(a, grid, c->stream);
+    else launch_expand_t<true, false, false>(a, grid, c->stream);
+  } else {
+    if (tlc) launch_expand_t<false, true, false>(a, grid, c->stream);
+    else if (part) launch_expand_t<false, false, true>(a, grid, c->stream);
+    else launch_expand_t<false, false, false>(a, grid, c->stream);
+  }
+  HIPCHK(hipGetLastError());
+  return true;
+}
+
+// TLC -workers 1 order for the level just expanded: sort the new states by
+// their first-discovery key (parent position, successor ordinal).
+bool tlc_order_level(tlcg_ctx* c, u64 n_new) {
+  if (!n_new) return true;
+  const Layout& L = c->hm.L;
+  const u64 d = distinct_of(c);
+  k_gather_dkey<<<grid_for(n_new, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(n_new, c->d_slot_new,
+                                                                              c->d_dkey_slot, c->d_dk);
+  HIPCHK(hipGetLastError());
+  const int end_bit = std::min(64, bits_for(((d + n_new) << L.ord_bits) | ((1ull << L.ord_bits) - 1)));
+  size_t tmp = c->sort_tmp_bytes;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, c->d_states + d, c->d_st2,
+                                            (int)n_new, 0, end_bit, c->stream));
+  k_tlc_finish<<<grid_for(n_new, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
+      L, n_new, c->d_st2, c->d_dk2, c->d_states + d, c->d_parents + d, (u64)c->opts.rank << 56, c->d_ctr);
+  HIPCHK(hipGetLastError());
+  return true;
+}
+
+bool step_level(tlcg_ctx* c) {
+  if (c->status != TLCG_RUNNING) return true;
+  const HostModel& hm = c->hm;
+  const int depth = (int)c->level_base.size() - 1;
+  const u64 f0 = c->level_base[(size_t)depth - 1], f1 = c->level_base[(size_t)depth];
+  const u64 F = f1 - f0;
+  if (!F) {
+    c->status = TLCG_DONE;
+    return true;
+  }
+  const u64 d = distinct_of(c);
+  const u64 worst = F * (u64)hm.max_new_per_state;
+  const u64 est = F * (u64)std::min(hm.max_new_per_state, 4);
+  if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return false;
+  if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + est)) return false;
+  if (!ensure_scratch(c, std::min(worst, c->cap - d))) return false;
+  for (;;) {
+    if (!reset_ctr(c)) return false;
+    HIPCHK(hipEventRecord(c->e0, c->stream));
+    if (!launch_expand(c, f0, F, false)) return false;
+    HIPCHK(hipEventRecord(c->e1, c->stream));
+    if (c->opts.tlc_order) {
+      // n_new is needed on the host to size the sort
+      if (!read_ctr(c)) return false;
+      if (!c->h_ctr->overflow && !tlc_order_level(c, c->h_ctr->n_new)) return false;
+    }
+    HIPCHK(hipEventRecord(c->e2, c->stream));
+    if (!read_ctr(c)) return false;
+    float ms_exp = 0, ms_all = 0;
+    hipEventElapsedTime(&ms_exp, c->e0, c->e1);
+    hipEventElapsedTime(&ms_all, c->e0, c->e2);
+    c->expand_ms += ms_exp;
+    c->kernel_ms += ms_all;
+    const unsigned ovf = c->h_ctr->overflow;
+    if (!ovf) break;
+    // grow and redo the level from the committed levels
+    ++c->levels_redone;
+    if (ovf & OVF_STORE) {
+      if (!ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * (c->cap - d)))) return false;
+      if (!ensure_scratch(c, c->cap - d)) return false;
+    }
+    if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d)) return false;
+  }
+  const u64 n_new = c->h_ctr->n_new;
+  c->generated += c->h_ctr->generated;
+  if (n_new) c->level_base.push_back(d + n_new);
+  if (c->h_ctr->event != NO_EVENT) return resolve_event(c, c->h_ctr->event, depth);
+  if (!n_new) c->status = TLCG_DONE;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
+  if (!m || !out) return -1;
+  *out = nullptr;
+  tlcg_ctx* c = new tlcg_ctx();
+  c->model = *m;
+  if (o) c->opts = *o;
+  else std::memset(&c->opts, 0, sizeof c->opts);
+  if (c->opts.world <= 0) c->opts.world = 1;
+  if (c->opts.world > 64 || c->opts.rank < 0 || c->opts.rank >= c->opts.world) {
+    c->err = "rank/world out of range (world <= 64)";
+    *out = c;
+    return -2;
+  }
+  if (c->opts.tlc_order && c->opts.world != 1) {
+    c->err = "TLC-order mode needs world == 1";
+    *out = c;
+    return -2;
+  }
+  if (!build_model(*m, &c->hm, &c->err)) {
+    *out = c;
+    return -3;
+  }
+  // partition key: `messages` alone when it is immutable (no Producer), so a
+  // state's whole successor graph stays on its owner rank; else the state.
+  const int part = c->opts.partition ? c->opts.partition : (c->hm.L.producer ? 2 : 1);
+  c->owner_mask = part == 1 ? c->hm.L.msgs_mask : ~0ull;
+  *out = c;
+  hipError_t e = hipSetDevice(c->opts.device);
+  if (e != hipSuccess) {
+    c->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return -4;
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
+      hipEventCreate(&c->e2) != hipSuccess) {
+    c->err = "stream/event creation failed";
+    return -4;
+  }
+  if (hipMalloc((void**)&c->d_ctr, sizeof(LevelCtr)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_ctr, sizeof(LevelCtr)) != hipSuccess) {
+    c->err = "counter allocation failed";
+    return -4;
+  }
+  if (c->opts.state_capacity && !ensure_store(c, c->opts.state_capacity)) return -5;
+  if (c->opts.log2_fpset_slots > 0 && !rebuild_fpset(c, c->opts.log2_fpset_slots, 0)) return -5;
+  return 0;
+}
+
+void tlcg_destroy(tlcg_ctx* c) {
+  if (!c) return;
+  if (c->stream) hipStreamSynchronize(c->stream);
+  hipFree(c->d_slots);
+  hipFree(c->d_dkey_slot);
+  hipFree(c->d_states);
+  hipFree(c->d_parents);
+  hipFree(c->d_slot_new);
+  hipFree(c->d_dk);
+  hipFree(c->d_dk2);
+  hipFree(c->d_st2);
+  hipFree(c->d_sort_tmp);
+  hipFree(c->d_outbox);
+  hipFree(c->d_inbox);
+  hipFree(c->d_ctr);
+  if (c->h_ctr) hipHostFree(c->h_ctr);
+  if (c->e0) hipEventDestroy(c->e0);
+  if (c->e1) hipEventDestroy(c->e1);
+  if (c->e2) hipEventDestroy(c->e2);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* tlcg_last_error(const tlcg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* tlcg_stream(tlcg_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
+  if (!c || !c->stream) return -1;
+  if (!run_init(c)) return -10;
+  c->inited = true;
+  fill_stats(c, st);
+  return 0;
+}
+
+int tlcg_step_level(tlcg_ctx* c, tlcg_stats* st) {
+  if (!c || !c->inited) return -1;
+  if (c->opts.world != 1) {
+    c->err = "tlcg_step_level is for world == 1; use tlcg_expand/absorb/end_level";
+    return -2;
+  }
+  if (!step_level(c)) return -10;
+  fill_stats(c, st);
+  return 0;
+}
+
+int tlcg_run(tlcg_ctx* c, tlcg_stats* st) {
+  int r = tlcg_init(c, st);
+  if (r) return r;
+  while (c->status == TLCG_RUNNING) {
+    r = tlcg_step_level(c, st);
+    if (r) return r;
+  }
+  fill_stats(c, st);
+  return 0;
+}
+
+int tlcg_level_sizes(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
+  if (!c) return -1;
+  const int depth = c->level_base.empty() ? 0 : (int)c->level_base.size() - 1;
+  for (int i = 0; i < depth && i < cap; ++i) out[i] = c->level_base[(size_t)i + 1] - c->level_base[(size_t)i];
+  if (n) *n = depth;
+  return 0;
+}
+
+int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref) {
+  if (!c || gidx >= distinct_of(c)) return -1;
+  u64 s = 0, p = 0;
+  if (!state_at(c, gidx, &s, &p)) return -10;
+  if (state) *state = s;
+  if (parent_ref) *parent_ref = p;
+  return 0;
+}
+
+int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
+  if (!c || first + n > distinct_of(c)) return -1;
+  if (n && hipMemcpy(out, c->d_states + first, n * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+    c->err = "copy failed";
+    return -10;
+  }
+  return 0;
+}
+
+int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len) {
+  if (!c) return -1;
+  if (c->ev_word == NO_EVENT) {
+    c->err = "no violation to trace";
+    return -2;
+  }
+  const Layout& L = c->hm.L;
+  const u64 ordmask = (1ull << L.ord_bits) - 1;
+  std::vector<u64> st;
+  std::vector<int> act;
+  if (c->ev_level == 0) {
+    st.push_back(c->ev_state);
+    act.push_back(TLCG_ACT_INIT);
+  } else {
+    if (c->ev_parent_gidx == NO_PARENT) {
+      c->err = "the trace crosses ranks: walk it with tlcg_state_at on each rank";
+      return -3;
+    }
+    u64 g = c->ev_parent_gidx;
+    for (;;) {
+      u64 s, p;
+      if (!state_at(c, g, &s, &p)) return -10;
+      st.push_back(s);
+      if (p == NO_PARENT) {
+        act.push_back(TLCG_ACT_INIT);
+        break;
+      }
+      if ((p >> 56) != (u64)c->opts.rank) {
+        c->err = "the trace crosses ranks";
+        return -3;
+      }
+      act.push_back(action_of_ordinal(L, (int)(p & ordmask)));
+      g = (p & ((1ull << 56) - 1)) >> L.ord_bits;
+    }
+    std::reverse(st.begin(), st.end());
+    std::reverse(act.begin(), act.end());
+    if (c->status == TLCG_VIOLATION || c->status == TLCG_INVARIANT_ERROR) {
+      st.push_back(c->ev_state);
+      act.push_back(c->ev_action);
+    }
+  }
+  const int n = (int)st.size();
+  for (int i = 0; i < n && i < cap; ++i) {
+    if (states) states[i] = st[(size_t)i];
+    if (actions) actions[i] = act[(size_t)i];
+  }
+  if (len) *len = n;
+  return 0;
+}
+
+int tlcg_owner(tlcg_ctx* c, uint64_t state) {
+  if (!c) return -1;
+  return (int)(((mix64(state & c->owner_mask) >> 32) * (u64)c->opts.world) >> 32);
+}
+
+// ---- partitioned levels (world > 1) ----
+
+int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
+  if (!c || !c->inited) return -1;
+  if (c->status != TLCG_RUNNING) {
+    fill_stats(c, st);
+    return 0;
+  }
+  const HostModel& hm = c->hm;
+  const int depth = (int)c->level_base.size() - 1;
+  const u64 f0 = depth ? c->level_base[(size_t)depth - 1] : 0;
+  const u64 F = depth ? c->level_base[(size_t)depth] - f0 : 0;
+  const u64 d = distinct_of(c);
+  const u64 est = F * (u64)std::min(hm.max_new_per_state, 4);
+  const u64 worst = F * (u64)hm.max_new_per_state;
+  if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return -10;
+  if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + est)) return -10;
+  // outbox: room for every successor of this level, split evenly with slack
+  const u64 per_dst = F ? worst / (u64)c->opts.world + worst / (u64)(2 * c->opts.world) + 1024 : 1024;
+  if (per_dst > c->outbox_cap) {
+    hipFree(c->d_outbox);
+    c->d_outbox = nullptr;
+    c->outbox_cap = 0;
+    if (!alloc_bytes(c, (void**)&c->d_outbox, per_dst * 16 * (u64)c->opts.world, "outbox")) return -10;
+    c->outbox_cap = per_dst;
+  }
+  c->absorbed_new = 0;
+  if (!reset_ctr(c)) return -10;
+  if (F) {
+    if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
+    if (!launch_expand(c, f0, F, true)) return -10;
+    if (hipEventRecord(c->e1, c->stream) != hipSuccess) return -10;
+  }
+  if (!read_ctr(c)) return -10;
+  if (F) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->e0, c->e1);
+    c->expand_ms += ms;
+    c->kernel_ms += ms;
+  }
+  if (c->h_ctr->overflow) {
+    c->err = "partitioned level overflowed its FPSet / store / outbox; size them up front (opts)";
+    return -11;
+  }
+  c->generated += c->h_ctr->generated;
+  fill_stats(c, st);
+  return 0;
+}
+
+int tlcg_outbox(tlcg_ctx* c, int32_t dst, void** dev_records, uint64_t* n_records) {
+  if (!c || dst < 0 || dst >= c->opts.world) return -1;
+  if (dev_records) *dev_records = c->d_outbox ? (void*)(c->d_outbox + 2 * (u64)dst * c->outbox_cap) : nullptr;
+  if (n_records) *n_records = dst == c->opts.rank ? 0 : c->h_ctr->n_out[dst];
+  return 0;
+}
+
+int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records) {
+  if (!c) return -1;
+  if (n_records > c->inbox_cap) {
+    hipFree(c->d_inbox);
+    c->d_inbox = nullptr;
+    c->inbox_cap = 0;
+    u64 ncap = std::max<u64>(n_records + n_records / 4, 4096);
+    if (!alloc_bytes(c, (void**)&c->d_inbox, ncap * 16, "inbox")) return -10;
+    c->inbox_cap = ncap;
+  }
+  if (dev_records) *dev_records = c->d_inbox;
+  return 0;
+}
+
+int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
+  if (!c || n_records > c->inbox_cap) return -1;
+  if (c->status != TLCG_RUNNING || !n_records) {
+    fill_stats(c, st);
+    return 0;
+  }
+  const u64 d = distinct_of(c);
+  const u64 local_new = c->h_ctr->n_new;  // appended by the expand (ctr not reset)
+  if (!ensure_store(c, d + local_new + n_records)) return -10;
+  if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + local_new + n_records)) return -10;
+  if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
+  k_absorb<<<grid_for(n_records, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
+      c->hm.L, c->d_inbox, n_records, c->d_slots, c->log2, c->d_states + d, c->d_parents + d, c->cap - d, c->d_ctr);
+  if (hipGetLastError() != hipSuccess) return -10;
+  if (hipEventRecord(c->e1, c->stream) != hipSuccess) return -10;
+  if (!read_ctr(c)) return -10;
+  float ms = 0;
+  hipEventElapsedTime(&ms, c->e0, c->e1);
+  c->kernel_ms += ms;
+  if (c->h_ctr->overflow) {
+    c->err = "absorb overflowed its FPSet / store; size them up front (opts)";
+    return -11;
+  }
+  fill_stats(c, st);
+  return 0;
+}
+
+int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st) {
+  if (!c) return -1;
+  if (c->status == TLCG_RUNNING) {
+    const int depth = (int)c->level_base.size() - 1;
+    const u64 n_new = c->h_ctr->n_new;
+    const u64 d = distinct_of(c);
+    c->level_base.push_back(d + n_new);  // empty levels kept (see run_init)
+    if (c->h_ctr->event != NO_EVENT) {
+      if (!resolve_event(c, c->h_ctr->event, depth)) return -10;
+    }
+  }
+  fill_stats(c, st);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,321 @@
+"""ctypes binding of libtlcgpu.so (include/tlcgpu.h) -- the MI355X checker.
+
+This is the Python face of the C ABI, used by bench.py, __graft_entry__ and the
+tests.  It mirrors TLC's vocabulary: a `Model` is the constants a TLC cfg binds
+(/root/reference/compaction.cfg:2-11) plus its INVARIANTS list (:25-31); a
+`Checker` runs the breadth-first safety check and reports TLC's numbers.
+
+There is no CPU fallback: if the HIP library is missing or no GPU is visible,
+constructing a Checker raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libtlcgpu.so"))
+
+MAX_SET = 63
+MAX_INV = 8
+
+INVARIANTS = ("TypeSafe", "CompactedLedgerLeak", "CompactionHorizonCorrectness", "DuplicateNullKeyMessage")
+ACTIONS = ("Producer", "CompactorPhaseOne", "CompactorPhaseTwoWrite", "CompactorPhaseTwoUpdateContext",
+           "CompactorPhaseTwoUpdateHorizon", "CompactorPhaseTwoPersistCusror", "CompactorPhaseTwoDeleteLedger",
+           "BrokerCrash", "Consumer", "Terminating")
+STATUS = {0: "running", 1: "ok", 2: "invariant", 3: "deadlock", 4: "action_error", 5: "invariant_error"}
+
+
+class tlcg_model(C.Structure):
+    _fields_ = [("msg_sent_limit", C.c_int32), ("compaction_times_limit", C.c_int32),
+                ("consume_times_limit", C.c_int32), ("max_crash_times", C.c_int32),
+                ("model_consumer", C.c_uint8), ("model_producer", C.c_uint8),
+                ("retain_null_key", C.c_uint8), ("check_deadlock", C.c_uint8),
+                ("n_keys", C.c_int32), ("n_values", C.c_int32),
+                ("keys", C.c_int64 * MAX_SET), ("values", C.c_int64 * MAX_SET),
+                ("n_invariants", C.c_int32), ("invariants", C.c_int32 * MAX_INV)]
+
+
+class tlcg_opts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("log2_fpset_slots", C.c_int32), ("state_capacity", C.c_uint64),
+                ("tlc_order", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32), ("partition", C.c_int32),
+                ("reserved", C.c_int32 * 7)]
+
+
+class tlcg_stats(C.Structure):
+    _fields_ = [("generated", C.c_uint64), ("distinct", C.c_uint64), ("frontier", C.c_uint64),
+                ("depth", C.c_int32), ("status", C.c_int32), ("invariant", C.c_int32), ("action", C.c_int32),
+                ("event_gidx", C.c_uint64), ("fp_collision_optimistic", C.c_double), ("kernel_ms", C.c_double),
+                ("expand_ms", C.c_double), ("levels_redone", C.c_uint64), ("reserved", C.c_uint64 * 4)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libtlcgpu.so and declare every exported signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libtlcgpu.so not built at {path}: run __graft_entry__.build()")
+    lib = C.CDLL(path)
+    P, U64, I32 = C.c_void_p, C.c_uint64, C.c_int32
+    M, O, S = C.POINTER(tlcg_model), C.POINTER(tlcg_opts), C.POINTER(tlcg_stats)
+    sig = {
+        "tlcg_abi_version": (C.c_int, []),
+        "tlcg_check_model": (C.c_int, [M, C.c_char_p, I32]),
+        "tlcg_state_bits": (C.c_int, [M]),
+        "tlcg_init_count": (U64, [M]),
+        "tlcg_create": (C.c_int, [M, O, C.POINTER(P)]),
+        "tlcg_destroy": (None, [P]),
+        "tlcg_last_error": (C.c_char_p, [P]),
+        "tlcg_init": (C.c_int, [P, S]),
+        "tlcg_step_level": (C.c_int, [P, S]),
+        "tlcg_run": (C.c_int, [P, S]),
+        "tlcg_level_sizes": (C.c_int, [P, C.POINTER(U64), I32, C.POINTER(I32)]),
+        "tlcg_trace": (C.c_int, [P, C.POINTER(U64), C.POINTER(I32), I32, C.POINTER(I32)]),
+        "tlcg_state_at": (C.c_int, [P, U64, C.POINTER(U64), C.POINTER(U64)]),
+        "tlcg_copy_states": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
+        "tlcg_ordinal_bits": (C.c_int, [M]),
+        "tlcg_action_of_ordinal": (C.c_int, [M, I32]),
+        "tlcg_decode": (C.c_int, [M, U64, C.c_char_p, I32]),
+        "tlcg_host_init_state": (U64, [M, U64]),
+        "tlcg_host_successors": (C.c_int, [M, U64, C.POINTER(U64), C.POINTER(I32), I32]),
+        "tlcg_host_check_invariants": (C.c_int, [M, U64]),
+        "tlcg_owner": (C.c_int, [P, U64]),
+        "tlcg_expand": (C.c_int, [P, S]),
+        "tlcg_outbox": (C.c_int, [P, I32, C.POINTER(P), C.POINTER(U64)]),
+        "tlcg_inbox": (C.c_int, [P, U64, C.POINTER(P)]),
+        "tlcg_absorb": (C.c_int, [P, U64, S]),
+        "tlcg_end_level": (C.c_int, [P, S]),
+        "tlcg_stream": (P, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+@dataclass
+class Model:
+    """Constants of compaction.tla:10-18 as a TLC cfg binds them."""
+    msg_sent_limit: int = 3          # MessageSentLimit
+    compaction_times_limit: int = 3  # CompactionTimesLimit
+    consume_times_limit: int = 2     # ConsumeTimesLimit
+    max_crash_times: int = 1         # MaxCrashTimes
+    model_consumer: bool = False     # ModelConsumer
+    model_producer: bool = False     # ModelProducer
+    retain_null_key: bool = True     # RetainNullKey
+    key_space: Sequence[int] = (1, 2)
+    value_space: Sequence[int] = (1, 2)
+    invariants: Sequence[str] = ("TypeSafe", "CompactionHorizonCorrectness")
+    check_deadlock: bool = True
+
+    def to_c(self) -> tlcg_model:
+        m = tlcg_model()
+        m.msg_sent_limit = self.msg_sent_limit
+        m.compaction_times_limit = self.compaction_times_limit
+        m.consume_times_limit = self.consume_times_limit
+        m.max_crash_times = self.max_crash_times
+        m.model_consumer = int(bool(self.model_consumer))
+        m.model_producer = int(bool(self.model_producer))
+        m.retain_null_key = int(bool(self.retain_null_key))
+        m.check_deadlock = int(bool(self.check_deadlock))
+        if len(self.key_space) > MAX_SET or len(self.value_space) > MAX_SET:
+            raise ValueError("KeySpace/ValueSpace larger than 63 elements")
+        m.n_keys = len(self.key_space)
+        m.n_values = len(self.value_space)
+        for i, k in enumerate(self.key_space):
+            m.keys[i] = int(k)
+        for i, v in enumerate(self.value_space):
+            m.values[i] = int(v)
+        if len(self.invariants) > MAX_INV:
+            raise ValueError("too many invariants")
+        m.n_invariants = len(self.invariants)
+        for i, name in enumerate(self.invariants):
+            if name not in INVARIANTS:
+                raise ValueError(f"unknown invariant {name}")
+            m.invariants[i] = INVARIANTS.index(name)
+        return m
+
+    def oracle_args(self) -> List[str]:
+        """Command-line of oracle/build/tlc_oracle for the same constants (tests only)."""
+        return ["-N", str(self.msg_sent_limit), "-C", str(self.compaction_times_limit),
+                "-K", str(self.max_crash_times), "-ctl", str(self.consume_times_limit),
+                "-keys", ",".join(map(str, self.key_space)) or "", "-values",
+                ",".join(map(str, self.value_space)) or "", "-retain", str(int(self.retain_null_key)),
+                "-producer", str(int(self.model_producer)), "-consumer", str(int(self.model_consumer)),
+                "-inv", ",".join(self.invariants)] + ([] if self.check_deadlock else ["-nodeadlock"])
+
+
+def check_model(model: Model) -> Optional[str]:
+    """ASSUME (compaction.tla:25-35) + packing; None if fine, else the message."""
+    lib = load_library()
+    buf = C.create_string_buffer(512)
+    m = model.to_c()
+    return None if lib.tlcg_check_model(C.byref(m), buf, 512) == 0 else buf.value.decode()
+
+
+def state_bits(model: Model) -> int:
+    m = model.to_c()
+    return load_library().tlcg_state_bits(C.byref(m))
+
+
+def init_count(model: Model) -> int:
+    m = model.to_c()
+    return load_library().tlcg_init_count(C.byref(m))
+
+
+def decode(model: Model, state: int) -> str:
+    lib = load_library()
+    m = model.to_c()
+    buf = C.create_string_buffer(1 << 16)
+    n = lib.tlcg_decode(C.byref(m), C.c_uint64(state), buf, len(buf))
+    if n < 0:
+        raise ValueError("bad model")
+    return buf.value.decode()
+
+
+def host_init_state(model: Model, idx: int) -> int:
+    m = model.to_c()
+    return load_library().tlcg_host_init_state(C.byref(m), idx)
+
+
+def host_successors(model: Model, state: int) -> List[Tuple[str, int]]:
+    lib = load_library()
+    m = model.to_c()
+    cap = 8192
+    out = (C.c_uint64 * cap)()
+    acts = (C.c_int32 * cap)()
+    n = lib.tlcg_host_successors(C.byref(m), C.c_uint64(state), out, acts, cap)
+    if n < 0:
+        raise RuntimeError("evaluation error")
+    return [(ACTIONS[acts[i]], out[i]) for i in range(n)]
+
+
+def host_check_invariants(model: Model, state: int) -> int:
+    m = model.to_c()
+    return load_library().tlcg_host_check_invariants(C.byref(m), C.c_uint64(state))
+
+
+@dataclass
+class Result:
+    status: str
+    generated: int
+    distinct: int
+    depth: int
+    left_on_queue: int
+    levels: List[int] = field(default_factory=list)
+    invariant: Optional[str] = None
+    action: Optional[str] = None
+    collision_optimistic: float = 0.0
+    kernel_ms: float = 0.0
+    expand_ms: float = 0.0
+    levels_redone: int = 0
+    trace: List[Tuple[str, int]] = field(default_factory=list)
+
+
+class Checker:
+    """One checking context on one GPU (libtlcgpu tlcg_ctx)."""
+
+    def __init__(self, model: Model, device: int = 0, log2_fpset_slots: int = 0, state_capacity: int = 0,
+                 tlc_order: bool = False, rank: int = 0, world: int = 1, partition: int = 0):
+        self.lib = load_library()
+        self.model = model
+        self._m = model.to_c()
+        o = tlcg_opts()
+        o.device, o.log2_fpset_slots, o.state_capacity = device, log2_fpset_slots, state_capacity
+        o.tlc_order, o.rank, o.world, o.partition = int(tlc_order), rank, world, partition
+        self._o = o
+        self.ctx = C.c_void_p()
+        rc = self.lib.tlcg_create(C.byref(self._m), C.byref(o), C.byref(self.ctx))
+        if rc != 0:
+            msg = self.lib.tlcg_last_error(self.ctx).decode() if self.ctx else "tlcg_create failed"
+            self.close()
+            raise RuntimeError(f"tlcg_create: {msg} ({rc})")
+        self.stats = tlcg_stats()
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.tlcg_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.lib.tlcg_last_error(self.ctx).decode()} ({rc})")
+
+    def init(self):
+        self._chk(self.lib.tlcg_init(self.ctx, C.byref(self.stats)), "tlcg_init")
+        return self.stats
+
+    def step_level(self):
+        self._chk(self.lib.tlcg_step_level(self.ctx, C.byref(self.stats)), "tlcg_step_level")
+        return self.stats
+
+    def run_raw(self):
+        """tlcg_run only (no host work after it): for timing."""
+        self._chk(self.lib.tlcg_run(self.ctx, C.byref(self.stats)), "tlcg_run")
+        return self.stats
+
+    def level_sizes(self) -> List[int]:
+        buf = (C.c_uint64 * 65536)()
+        n = C.c_int32()
+        self._chk(self.lib.tlcg_level_sizes(self.ctx, buf, 65536, C.byref(n)), "tlcg_level_sizes")
+        return [buf[i] for i in range(min(n.value, 65536))]
+
+    def trace(self) -> List[Tuple[str, int]]:
+        cap = 1 << 16
+        st = (C.c_uint64 * cap)()
+        ac = (C.c_int32 * cap)()
+        n = C.c_int32()
+        self._chk(self.lib.tlcg_trace(self.ctx, st, ac, cap, C.byref(n)), "tlcg_trace")
+        return [("Init" if ac[i] < 0 else ACTIONS[ac[i]], st[i]) for i in range(n.value)]
+
+    def copy_states(self, first: int, n: int) -> List[int]:
+        buf = (C.c_uint64 * max(n, 1))()
+        self._chk(self.lib.tlcg_copy_states(self.ctx, first, n, buf), "tlcg_copy_states")
+        return list(buf[:n])
+
+    def state_at(self, gidx: int) -> Tuple[int, int]:
+        s, p = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.tlcg_state_at(self.ctx, gidx, C.byref(s), C.byref(p)), "tlcg_state_at")
+        return s.value, p.value
+
+    def result(self, with_trace: bool = True) -> Result:
+        s = self.stats
+        status = STATUS[s.status]
+        r = Result(status=status, generated=s.generated, distinct=s.distinct, depth=s.depth,
+                   left_on_queue=0 if status == "ok" else s.frontier, levels=self.level_sizes(),
+                   collision_optimistic=s.fp_collision_optimistic, kernel_ms=s.kernel_ms,
+                   expand_ms=s.expand_ms, levels_redone=s.levels_redone)
+        if s.invariant >= 0:
+            r.invariant = self.model.invariants[s.invariant]
+        if s.action >= 0:
+            r.action = ACTIONS[s.action]
+        if with_trace and status not in ("ok", "running"):
+            r.trace = self.trace()
+        return r
+
+    def run(self, with_trace: bool = True) -> Result:
+        self.run_raw()
+        return self.result(with_trace)
+
+
+def run(model: Model, **kw) -> Result:
+    """Convenience: check `model` on one GPU."""
+    ck = Checker(model, **kw)
+    try:
+        return ck.run()
+    finally:
+        ck.close()
