@@ -1,0 +1,201 @@
+"""Benchmark: distinct states/s of the BFS safety check of compaction.tla on the
+scaled cfg (BASELINE.json metric), on 1..8 MI355X.
+
+A step = one complete model check of the G9 config (SURVEY 8(d):
+KeySpace = ValueSpace = {1..15}, MessageSentLimit = 3, CompactionTimesLimit = 3,
+MaxCrashTimes = 1, RetainNullKey, no producer/consumer -> 1,040,187,392
+distinct states, 1,392,508,928 generated, depth 20): FPSet cleared, Init,
+then every BFS level until the queue is empty.  Inputs are the constants;
+everything lives in HBM.  With N GPUs the same job is split across N ranks
+(strong scaling), the FPSet hash-partitioned by owner (dist.py).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config g9|m8|s]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pulsar-tlaplus_amd", "python"))
+
+CONFIGS = {
+    "g9": dict(keys=15, distinct=1_040_187_392, generated=1_392_508_928, depth=20),
+    "m8": dict(keys=10, distinct=109_836_782, generated=147_039_563, depth=20),
+    "s": dict(keys=2, distinct=45_198, generated=60_507, depth=20),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# algorithmic bytes per distinct state of the fused expand kernel:
+# read the parent word (8 B) + write the new word and its parent entry (16 B)
+# + one 8-B FPSet slot probe per non-stuttering successor (g'/d of them)
+BYTES_PER_STATE_WORD = 8
+
+
+def model_for(cfg):
+    import tlcgpu
+    k = CONFIGS[cfg]["keys"]
+    return tlcgpu.Model(key_space=range(1, k + 1), value_space=range(1, k + 1))
+
+
+def algorithmic_bytes(distinct, generated, n_init, selfloops):
+    probes = generated - n_init - selfloops  # successors inserted into the FPSet
+    return BYTES_PER_STATE_WORD * (distinct + 2 * (distinct - n_init) + probes)
+
+
+def selfloops_per_m(model):
+    import tlcgpu
+    seen, todo, loops = set(), [tlcgpu.host_init_state(model, 0)], 0
+    while todo:
+        s = todo.pop()
+        if s in seen:
+            continue
+        seen.add(s)
+        for _, t in tlcgpu.host_successors(model, s):
+            loops += t == s
+            todo.append(t)
+    return loops
+
+
+def cpu_baseline(cfg, seconds_target=12.0):
+    """The oracle (TEST INFRASTRUCTURE, single thread) on a bounded sample of the
+    same workload: the first n initial message sequences of the cfg."""
+    oracle = os.path.join(ROOT, "oracle", "build", "tlc_oracle")
+    if not os.path.exists(oracle):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    k = CONFIGS[cfg]["keys"]
+    keys = ",".join(str(i) for i in range(1, k + 1))
+    n_m = 4096
+    while True:
+        t = time.time()
+        out = subprocess.run([oracle, "-keys", keys, "-values", keys, "-init-lo", "0", "-init-hi", str(n_m),
+                              "-notrace"], check=True, capture_output=True, text=True).stdout
+        wall = time.time() - t
+        r = json.loads(out)
+        if r["seconds"] >= seconds_target / 4 or n_m >= (k + 1) ** 6:
+            break
+        n_m = min(n_m * 4, (k + 1) ** 6)
+    return dict(value=r["distinct"] / r["seconds"], unit="distinct states/s", cores=1, kind="port",
+                sample=f"oracle/tlc_oracle (C restatement, 1 thread) on the first {n_m} of {(k + 1) ** 6} initial "
+                       f"message sequences of the {cfg.upper()} cfg: {r['distinct']} distinct states in "
+                       f"{r['seconds']:.2f} s (TLC itself is not installed on the GPU host)",
+                wall_s=round(wall, 2))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="g9", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import tlcgpu
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
+
+    cfg = CONFIGS[args.config]
+    model = model_for(args.config)
+    per_rank = cfg["distinct"] // world + 1
+    log2 = max(16, (2 * per_rank - 1).bit_length())
+    cap = int(per_rank * 1.08) + 2 * (cfg["distinct"] // 12) // world + (1 << 20)
+    import dist as tdist
+    eng = tdist.GpuEngine(model, rank, world, local_rank, log2_fpset_slots=log2, state_capacity=cap)
+    assert eng.closed
+
+    def step():
+        return eng.run_closed()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    expand_ms = kernel_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+        expand_ms += st.expand_ms
+        kernel_ms += st.kernel_ms
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    levels = eng.level_sizes()
+    launches = len(levels)  # one expand launch per level (the last finds nothing new)
+    local = [st.generated, st.distinct]
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor(local, dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        local = [int(x) for x in c.tolist()]
+        e = torch.tensor([expand_ms, kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        expand_ms, kernel_ms = [float(x) for x in e.tolist()]
+    generated, distinct = local
+    if (generated, distinct) != (cfg["generated"], cfg["distinct"]):
+        raise SystemExit(f"count mismatch: {generated} generated, {distinct} distinct, want {cfg}")
+    if rank != 0:
+        if distributed:
+            dist.destroy_process_group()
+        return
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = distinct * args.steps / elapsed
+    n_init = (cfg["keys"] + 1) ** 6
+    # stuttering successors (no FPSet probe): counted on one message sequence,
+    # every sequence has the same compactor graph (SURVEY App.A.1)
+    selfloops = n_init * selfloops_per_m(model)
+    bytes_step = algorithmic_bytes(distinct, generated, n_init, selfloops) / world  # per rank
+    expand_ms_step = expand_ms / args.steps
+    achieved = bytes_step / (expand_ms_step * 1e-3) / 1e9
+    roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                    kernel="k_expand", launches_per_step=launches,
+                    avg_launch_ms=round(expand_ms_step / launches, 4),
+                    bytes_per_distinct=round(algorithmic_bytes(distinct, generated, n_init, selfloops) / distinct, 2))
+    line = {
+        "metric": "distinct states/sec, compaction.tla scaled cfg, 1/2/4/8 MI355X vs host TLC",
+        "value": round(value, 1),
+        "unit": "distinct states/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: the model's own state space (no external data)",
+        "config": {"workload": f"compaction.tla BFS, {args.config.upper()} cfg: KeySpace = ValueSpace = "
+                               f"{{1..{cfg['keys']}}}, MessageSentLimit 3, CompactionTimesLimit 3, MaxCrashTimes 1, "
+                               f"RetainNullKey, no producer/consumer",
+                   "distinct": distinct, "generated": generated, "depth": len(levels),
+                   "parallelism": f"fpset-partition{world}", "fpset_slots_log2": log2,
+                   "gpu_kernel_ms_per_step": round(kernel_ms / args.steps, 3)},
+        "roofline": roofline,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.config)
+    print(json.dumps(line), flush=True)
+    eng.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

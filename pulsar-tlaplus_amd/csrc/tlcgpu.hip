@@ -343,7 +343,8 @@ struct tlcg_ctx {
   u64 outbox_cap = 0;  // records per destination
   u64* d_inbox = nullptr;
   u64 inbox_cap = 0;
-  u64 absorbed_new = 0;
+  u64 pending = 0;      // states appended to the current level, not yet committed
+  bool closed = false;  // partition by immutable `messages`: successors never leave the rank
   // counters
   LevelCtr* d_ctr = nullptr;
   LevelCtr* h_ctr = nullptr;
@@ -403,7 +404,7 @@ bool ensure_store(tlcg_ctx* c, u64 need) {
   u64 *ns = nullptr, *np = nullptr;
   if (!alloc_bytes(c, (void**)&ns, ncap * 8, "state store")) return false;
   if (!alloc_bytes(c, (void**)&np, ncap * 8, "parent log")) { hipFree(ns); return false; }
-  const u64 keep = distinct_of(c);
+  const u64 keep = std::min<u64>(c->cap, distinct_of(c) + c->pending);
   if (keep) {
     HIPCHK(hipMemcpyAsync(ns, c->d_states, keep * 8, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(np, c->d_parents, keep * 8, hipMemcpyDeviceToDevice, c->stream));
@@ -445,12 +446,13 @@ bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
   return true;
 }
 
-// keep the FPSet load <= 1/2 for `need` states
+// keep the FPSet load <= 1/2 for `need` states; re-inserts the stored ones
+// (committed levels + what the current level appended so far)
 bool ensure_fpset(tlcg_ctx* c, u64 need) {
   int l = std::max(c->log2, 16);
   while ((1ull << l) < 2 * need && l < 40) ++l;
   if (c->d_slots && l == c->log2) return true;
-  return rebuild_fpset(c, l, distinct_of(c));
+  return rebuild_fpset(c, l, distinct_of(c) + c->pending);
 }
 
 bool ensure_scratch(tlcg_ctx* c, u64 n) {
@@ -778,6 +780,7 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
   // state's whole successor graph stays on its owner rank; else the state.
   const int part = c->opts.partition ? c->opts.partition : (c->hm.L.producer ? 2 : 1);
   c->owner_mask = part == 1 ? c->hm.L.msgs_mask : ~0ull;
+  c->closed = c->opts.world == 1 || (part == 1 && !c->hm.L.producer);
   *out = c;
   hipError_t e = hipSetDevice(c->opts.device);
   if (e != hipSuccess) {
@@ -837,8 +840,8 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
 
 int tlcg_step_level(tlcg_ctx* c, tlcg_stats* st) {
   if (!c || !c->inited) return -1;
-  if (c->opts.world != 1) {
-    c->err = "tlcg_step_level is for world == 1; use tlcg_expand/absorb/end_level";
+  if (!c->closed) {
+    c->err = "successors can leave this rank: use tlcg_expand/outbox/inbox/absorb/end_level";
     return -2;
   }
   if (!step_level(c)) return -10;
@@ -964,7 +967,7 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
     if (!alloc_bytes(c, (void**)&c->d_outbox, per_dst * 16 * (u64)c->opts.world, "outbox")) return -10;
     c->outbox_cap = per_dst;
   }
-  c->absorbed_new = 0;
+  c->pending = 0;
   if (!reset_ctr(c)) return -10;
   if (F) {
     if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
@@ -983,6 +986,7 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
     return -11;
   }
   c->generated += c->h_ctr->generated;
+  c->pending = c->h_ctr->n_new;
   fill_stats(c, st);
   return 0;
 }
@@ -1016,6 +1020,7 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
   }
   const u64 d = distinct_of(c);
   const u64 local_new = c->h_ctr->n_new;  // appended by the expand (ctr not reset)
+  c->pending = local_new;
   if (!ensure_store(c, d + local_new + n_records)) return -10;
   if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + local_new + n_records)) return -10;
   if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
@@ -1042,6 +1047,7 @@ int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st) {
     const u64 n_new = c->h_ctr->n_new;
     const u64 d = distinct_of(c);
     c->level_base.push_back(d + n_new);  // empty levels kept (see run_init)
+    c->pending = 0;
     if (c->h_ctr->event != NO_EVENT) {
       if (!resolve_event(c, c->h_ctr->event, depth)) return -10;
     }

@@ -1,0 +1,171 @@
+"""Multi-GPU BFS: one process (rank) per MI355X, FPSet hash-partitioned by owner.
+
+This is the distributed counterpart of TLC's FPSetManager (tlc2.tool.fp,
+fingerprint-partitioned FPSet): every rank owns the states whose owner hash
+(mix64 of the partition key) maps to it.
+
+Two regimes, chosen by libtlcgpu from the model:
+
+* closed partition -- with ModelProducer = FALSE no action writes `messages`
+  (compaction.tla:87,100,132,139,145,151,165,182,186,214), so keying the owner
+  hash on `messages` keeps every successor on its parent's rank.  Each rank
+  runs its BFS to completion with no data-path collective; one all-reduce
+  combines the counts (distinct/generated sum, depth max, first error).
+* open partition -- otherwise (Producer appends to `messages`) each level is
+  expand -> all-to-all of 16-byte {state, parent_ref} records to their owners
+  (RCCL over xGMI with the nccl backend) -> absorb -> all-reduce of the level
+  counters to decide termination.
+
+`Engine` is the per-rank face of include/tlcgpu.h's partitioned API; the GPU
+engine wraps libtlcgpu, the tests plug a CPU stand-in into the same driver.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+import tlcgpu
+
+STATUS_RUNNING, STATUS_DONE = 0, 1
+
+
+@dataclass
+class DistResult:
+    status: str
+    generated: int
+    distinct: int
+    depth: int
+    levels: List[int]
+    kernel_ms: float
+    expand_ms: float
+    closed: bool
+
+
+_hip = None
+
+
+def _hip_memcpy(dst: int, src: int, nbytes: int):
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipMemcpy.restype = C.c_int
+    if nbytes and _hip.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, 3) != 0:  # DeviceToDevice
+        raise RuntimeError("hipMemcpy failed")
+
+
+class GpuEngine:
+    """One rank's libtlcgpu context (the partitioned C-ABI)."""
+
+    def __init__(self, model: tlcgpu.Model, rank: int, world: int, device: int, **opts):
+        self.ck = tlcgpu.Checker(model, device=device, rank=rank, world=world, **opts)
+        self.lib, self.ctx, self.stats = self.ck.lib, self.ck.ctx, self.ck.stats
+        self.world, self.rank, self.device = world, rank, device
+        self.closed = world == 1 or (not model.model_producer and opts.get("partition", 0) in (0, 1))
+
+    def run_closed(self) -> tlcgpu.tlcg_stats:
+        return self.ck.run_raw()
+
+    def init(self):
+        return self.ck.init()
+
+    def expand(self) -> List[int]:
+        self.ck._chk(self.lib.tlcg_expand(self.ctx, C.byref(self.stats)), "tlcg_expand")
+        counts = []
+        for dst in range(self.world):
+            p, n = C.c_void_p(), C.c_uint64()
+            self.lib.tlcg_outbox(self.ctx, dst, C.byref(p), C.byref(n))
+            counts.append(n.value)
+        return counts
+
+    def outbox(self, dst: int) -> torch.Tensor:
+        p, n = C.c_void_p(), C.c_uint64()
+        self.lib.tlcg_outbox(self.ctx, dst, C.byref(p), C.byref(n))
+        t = torch.empty((n.value, 2), dtype=torch.int64, device=f"cuda:{self.device}")
+        torch.cuda.synchronize(self.device)
+        _hip_memcpy(t.data_ptr(), p.value or 0, n.value * 16)
+        return t
+
+    def absorb(self, recs: torch.Tensor):
+        n = recs.shape[0]
+        p = C.c_void_p()
+        self.ck._chk(self.lib.tlcg_inbox(self.ctx, n, C.byref(p)), "tlcg_inbox")
+        torch.cuda.synchronize(self.device)
+        _hip_memcpy(p.value, recs.data_ptr(), n * 16)
+        self.ck._chk(self.lib.tlcg_absorb(self.ctx, n, C.byref(self.stats)), "tlcg_absorb")
+
+    def end_level(self):
+        self.ck._chk(self.lib.tlcg_end_level(self.ctx, C.byref(self.stats)), "tlcg_end_level")
+        return self.stats
+
+    def level_sizes(self) -> List[int]:
+        return self.ck.level_sizes()
+
+    def new_tensor(self, shape, dtype):
+        return torch.empty(shape, dtype=dtype, device=f"cuda:{self.device}")
+
+    def close(self):
+        self.ck.close()
+
+
+def _reduce_result(engine, stats, group, dev: torch.device) -> DistResult:
+    levels = engine.level_sizes()
+    depth_local = len(levels)
+    t = torch.tensor([stats.generated, stats.distinct], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    d = torch.tensor([depth_local], dtype=torch.int64, device=dev)
+    dist.all_reduce(d, op=dist.ReduceOp.MAX, group=group)
+    depth = int(d.item())
+    lv = torch.zeros(max(depth, 1), dtype=torch.int64, device=dev)
+    if levels:
+        lv[: len(levels)] = torch.tensor(levels, dtype=torch.int64, device=dev)
+    dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
+    # the first error in (level, rank) order wins; 0 = no error
+    st = int(stats.status)
+    code = torch.tensor([st if st >= 2 else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(code, op=dist.ReduceOp.MAX, group=group)
+    status = tlcgpu.STATUS[int(code.item())] if code.item() else "ok"
+    levels_all = [int(x) for x in lv.tolist()]
+    while levels_all and levels_all[-1] == 0:
+        levels_all.pop()
+    return DistResult(status=status, generated=int(t[0].item()), distinct=int(t[1].item()),
+                      depth=len(levels_all), levels=levels_all, kernel_ms=stats.kernel_ms,
+                      expand_ms=stats.expand_ms, closed=engine.closed)
+
+
+def run(engine, group=None, dev: Optional[torch.device] = None) -> DistResult:
+    """Model-check with every rank of `group` (engine = this rank's share)."""
+    dev = dev or torch.device("cpu")
+    world = dist.get_world_size(group)
+    if engine.closed:
+        stats = engine.run_closed()
+        return _reduce_result(engine, stats, group, dev)
+    stats = engine.init()
+    me = dist.get_rank(group)
+    lv0 = engine.level_sizes()
+    flags = torch.tensor([lv0[-1] if lv0 else 0, 1 if stats.status >= 2 else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
+    while not flags[1].item() and flags[0].item():
+        counts = engine.expand()
+        # all-to-all: counts, then the records (16 bytes each)
+        send_counts = torch.tensor(counts, dtype=torch.int64, device=dev)
+        recv_counts = torch.empty(world, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv_counts, send_counts, group=group)
+        rc = [int(x) for x in recv_counts.tolist()]
+        sends = [engine.outbox(d) if d != me else engine.new_tensor((0, 2), torch.int64) for d in range(world)]
+        send = torch.cat(sends, 0) if sends else engine.new_tensor((0, 2), torch.int64)
+        recv = engine.new_tensor((sum(rc), 2), torch.int64)
+        sc = [s.shape[0] for s in sends]
+        dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc, group=group)
+        if recv.shape[0]:
+            engine.absorb(recv)
+        stats = engine.end_level()
+        # global termination: any error, or no new state anywhere
+        lv = engine.level_sizes()
+        flags = torch.tensor([lv[-1] if lv else 0, 1 if stats.status >= 2 else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
+    return _reduce_result(engine, stats, group, dev)

@@ -1,0 +1,106 @@
+"""CPU: the product's packed encoding (model.h, compiled for the host inside
+libtlcgpu.so -- the same code the gfx950 kernels run) against the oracle.
+
+A plain Python BFS over tlcg_host_successors must reproduce the golden counts,
+per-level sizes and traces; decoded trace states must match the oracle's TLC
+text byte for byte.  No GPU call is made."""
+import pytest
+
+import tlcgpu
+from conftest import GOLDEN, model_of
+
+
+def host_bfs(m):
+    n = tlcgpu.init_count(m)
+    seen, order, parent, act = {}, [], [], []
+    for i in range(n):
+        s = tlcgpu.host_init_state(m, i)
+        seen[s] = len(order)
+        order.append(s)
+        parent.append(-1)
+        act.append("Init")
+        c = tlcgpu.host_check_invariants(m, s)
+        if c >= 0:
+            return dict(result="invariant", invariant=m.invariants[c >> 1], trace=[("Init", s)])
+    gen, levels, head = n, [n] if n else [], 0
+
+    def trace_to(k):
+        out = []
+        while k >= 0:
+            out.append((act[k], order[k]))
+            k = parent[k]
+        return out[::-1]
+
+    while head < len(order):
+        end = len(order)
+        for p in range(head, end):
+            succ = tlcgpu.host_successors(m, order[p])
+            if not succ and m.check_deadlock:
+                return dict(result="deadlock", trace=trace_to(p))
+            for a, t in succ:
+                gen += 1
+                if t not in seen:
+                    seen[t] = len(order)
+                    order.append(t)
+                    parent.append(p)
+                    act.append(a)
+                    c = tlcgpu.host_check_invariants(m, t)
+                    if c >= 0:
+                        return dict(result="invariant", invariant=m.invariants[c >> 1], trace=trace_to(len(order) - 1))
+        head = end
+        if len(order) > end:
+            levels.append(len(order) - end)
+    return dict(result="ok", generated=gen, distinct=len(order), depth=len(levels), levels=levels)
+
+
+CASES = ["S", "S_noretain", "S_consumer", "S_consumer_ctl0", "V_leak", "V_dup", "V_dup_producer", "D_N0_K1",
+         "D_N0_K0", "D_N0_K1_nodeadlock", "X_keys3_vals57", "X_producer_sparse", "X_C5_K2", "X_empty_spaces",
+         "R_C6_K3", "R_C1_K0"]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_host_encoding_bfs(case):
+    g = GOLDEN[case]
+    m = model_of(g["constants"])
+    r = host_bfs(m)
+    want = g["result"]
+    assert r["result"] == want["result"]
+    if want["result"] == "ok":
+        assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (
+            want["generated"], want["distinct"], want["depth"], want["levels"])
+    else:
+        assert [a for a, _ in r["trace"]] == [t["action"] for t in want["trace"]]
+        assert [tlcgpu.decode(m, s) for _, s in r["trace"]] == [t["state"] for t in want["trace"]]
+        if want["result"] == "invariant":
+            assert r["invariant"] == want["invariant"]
+
+
+def test_host_encoding_published_producer():
+    # compaction.tla:23: 253361 with the producer modelled (RetainNullKey = FALSE)
+    r = host_bfs(model_of(GOLDEN["P_published"]["constants"]))
+    assert r["distinct"] == 253361 and r["generated"] == GOLDEN["P_published"]["result"]["generated"]
+
+
+def test_state_bits():
+    assert tlcgpu.state_bits(tlcgpu.Model()) == 41
+    g9 = tlcgpu.Model(key_space=range(1, 16), value_space=range(1, 16))
+    assert tlcgpu.state_bits(g9) == 53  # SURVEY App.B: 55 with the (constant) consumeTimes field
+    assert tlcgpu.init_count(g9) == 16 ** 6
+
+
+def test_init_order_first_is_all_null():
+    m = tlcgpu.Model()
+    assert tlcgpu.decode(m, tlcgpu.host_init_state(m, 0)).startswith(
+        "/\\ messages = <<[id |-> 1, key |-> 0, value |-> 0], [id |-> 2, key |-> 0, value |-> 0]")
+    # message 1 varies fastest, its key faster than its value
+    assert "[id |-> 1, key |-> 1, value |-> 0]" in tlcgpu.decode(m, tlcgpu.host_init_state(m, 1))
+    assert "[id |-> 1, key |-> 0, value |-> 1]" in tlcgpu.decode(m, tlcgpu.host_init_state(m, 3))
+    assert "[id |-> 2, key |-> 1, value |-> 0]" in tlcgpu.decode(m, tlcgpu.host_init_state(m, 9))
+
+
+def test_phase_one_result_printing():
+    m = tlcgpu.Model(key_space=[2, 5], value_space=[1])
+    s = tlcgpu.host_init_state(m, 1 + 3 * 0 + 6 * 2)  # msg1 key 2, msg2 key 5
+    (a, t), = [x for x in tlcgpu.host_successors(m, s) if x[0] == "CompactorPhaseOne"]
+    txt = tlcgpu.decode(m, t)
+    assert "phaseOneResult = [latestForKey |-> (2 :> 1 @@ 5 :> 2), readPosition |-> 3]" in txt
