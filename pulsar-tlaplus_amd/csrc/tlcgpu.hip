@@ -348,6 +348,8 @@ struct tlcg_ctx {
   // counters
   LevelCtr* d_ctr = nullptr;
   LevelCtr* h_ctr = nullptr;
+  LevelCtr* d_aux = nullptr;  // counters of FPSet rebuilds (never the level's)
+  LevelCtr* h_aux = nullptr;
   // run state
   std::vector<u64> level_base;  // level_base[d] = gidx of the first state of level d
   u64 generated = 0;
@@ -433,12 +435,12 @@ bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
   HIPCHK(hipMemsetAsync(c->d_slots, 0, 8ull << log2, c->stream));
   if (c->d_dkey_slot) HIPCHK(hipMemsetAsync(c->d_dkey_slot, 0xFF, 8ull << log2, c->stream));
   if (n) {
-    HIPCHK(hipMemsetAsync(c->d_ctr, 0, sizeof(LevelCtr), c->stream));
-    k_reinsert<<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(c->d_states, n, c->d_slots, log2, c->d_ctr);
+    HIPCHK(hipMemsetAsync(c->d_aux, 0, sizeof(LevelCtr), c->stream));
+    k_reinsert<<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(c->d_states, n, c->d_slots, log2, c->d_aux);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->h_ctr, c->d_ctr, sizeof(LevelCtr), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_aux, c->d_aux, sizeof(LevelCtr), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->h_ctr->overflow) {
+    if (c->h_aux->overflow) {
       c->err = "FPSet rebuild overflowed";
       return false;
     }
@@ -699,6 +701,20 @@ bool tlc_order_level(tlcg_ctx* c, u64 n_new) {
   return true;
 }
 
+// expected new states of the next level: the last level's growth ratio (with
+// headroom), capped by the per-state bound
+u64 next_level_estimate(const tlcg_ctx* c, u64 F) {
+  const HostModel& hm = c->hm;
+  const size_t n = c->level_base.size();
+  double ratio = 2.0;
+  if (n >= 3) {
+    const u64 prev = c->level_base[n - 2] - c->level_base[n - 3];
+    if (prev) ratio = std::max(ratio, 1.5 * (double)F / (double)prev);
+  }
+  ratio = std::min(ratio, (double)hm.max_new_per_state);
+  return (u64)(ratio * (double)F) + 1024;
+}
+
 bool step_level(tlcg_ctx* c) {
   if (c->status != TLCG_RUNNING) return true;
   const HostModel& hm = c->hm;
@@ -711,7 +727,7 @@ bool step_level(tlcg_ctx* c) {
   }
   const u64 d = distinct_of(c);
   const u64 worst = F * (u64)hm.max_new_per_state;
-  const u64 est = F * (u64)std::min(hm.max_new_per_state, 4);
+  const u64 est = next_level_estimate(c, F);
   if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return false;
   if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + est)) return false;
   if (!ensure_scratch(c, std::min(worst, c->cap - d))) return false;
@@ -794,7 +810,9 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
     return -4;
   }
   if (hipMalloc((void**)&c->d_ctr, sizeof(LevelCtr)) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_ctr, sizeof(LevelCtr)) != hipSuccess) {
+      hipHostMalloc((void**)&c->h_ctr, sizeof(LevelCtr)) != hipSuccess ||
+      hipMalloc((void**)&c->d_aux, sizeof(LevelCtr)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_aux, sizeof(LevelCtr)) != hipSuccess) {
     c->err = "counter allocation failed";
     return -4;
   }
@@ -818,7 +836,9 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_outbox);
   hipFree(c->d_inbox);
   hipFree(c->d_ctr);
+  hipFree(c->d_aux);
   if (c->h_ctr) hipHostFree(c->h_ctr);
+  if (c->h_aux) hipHostFree(c->h_aux);
   if (c->e0) hipEventDestroy(c->e0);
   if (c->e1) hipEventDestroy(c->e1);
   if (c->e2) hipEventDestroy(c->e2);
@@ -954,36 +974,45 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
   const u64 f0 = depth ? c->level_base[(size_t)depth - 1] : 0;
   const u64 F = depth ? c->level_base[(size_t)depth] - f0 : 0;
   const u64 d = distinct_of(c);
-  const u64 est = F * (u64)std::min(hm.max_new_per_state, 4);
+  const u64 est = next_level_estimate(c, F);
   const u64 worst = F * (u64)hm.max_new_per_state;
+  c->pending = 0;
   if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return -10;
   if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + est)) return -10;
-  // outbox: room for every successor of this level, split evenly with slack
-  const u64 per_dst = F ? worst / (u64)c->opts.world + worst / (u64)(2 * c->opts.world) + 1024 : 1024;
-  if (per_dst > c->outbox_cap) {
-    hipFree(c->d_outbox);
-    c->d_outbox = nullptr;
-    c->outbox_cap = 0;
-    if (!alloc_bytes(c, (void**)&c->d_outbox, per_dst * 16 * (u64)c->opts.world, "outbox")) return -10;
-    c->outbox_cap = per_dst;
-  }
-  c->pending = 0;
-  if (!reset_ctr(c)) return -10;
-  if (F) {
-    if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
-    if (!launch_expand(c, f0, F, true)) return -10;
-    if (hipEventRecord(c->e1, c->stream) != hipSuccess) return -10;
-  }
-  if (!read_ctr(c)) return -10;
-  if (F) {
-    float ms = 0;
-    hipEventElapsedTime(&ms, c->e0, c->e1);
-    c->expand_ms += ms;
-    c->kernel_ms += ms;
-  }
-  if (c->h_ctr->overflow) {
-    c->err = "partitioned level overflowed its FPSet / store / outbox; size them up front (opts)";
-    return -11;
+  // outbox: an even split of the expected successors, with slack; grows on overflow
+  u64 per_dst = F ? 2 * est / (u64)c->opts.world + 1024 : 1024;
+  for (;;) {
+    if (per_dst > c->outbox_cap) {
+      hipFree(c->d_outbox);
+      c->d_outbox = nullptr;
+      c->outbox_cap = 0;
+      if (!alloc_bytes(c, (void**)&c->d_outbox, per_dst * 16 * (u64)c->opts.world, "outbox")) return -10;
+      c->outbox_cap = per_dst;
+    }
+    if (!reset_ctr(c)) return -10;
+    if (F) {
+      if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
+      if (!launch_expand(c, f0, F, true)) return -10;
+      if (hipEventRecord(c->e1, c->stream) != hipSuccess) return -10;
+    }
+    if (!read_ctr(c)) return -10;
+    if (F) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, c->e0, c->e1);
+      c->expand_ms += ms;
+      c->kernel_ms += ms;
+    }
+    const unsigned ovf = c->h_ctr->overflow;
+    if (!ovf) break;
+    // grow what overflowed and redo the expansion from the committed levels
+    ++c->levels_redone;
+    if (ovf & OVF_OUTBOX) {
+      u64 mx = 0;
+      for (int r = 0; r < c->opts.world; ++r) mx = std::max<u64>(mx, c->h_ctr->n_out[r]);
+      per_dst = std::max<u64>(2 * per_dst, mx + mx / 4);
+    }
+    if ((ovf & OVF_STORE) && !ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * (c->cap - d)))) return -10;
+    if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d)) return -10;
   }
   c->generated += c->h_ctr->generated;
   c->pending = c->h_ctr->n_new;
@@ -1020,22 +1049,32 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
   }
   const u64 d = distinct_of(c);
   const u64 local_new = c->h_ctr->n_new;  // appended by the expand (ctr not reset)
+  const LevelCtr before = *c->h_ctr;      // the level's counters after the expand
   c->pending = local_new;
   if (!ensure_store(c, d + local_new + n_records)) return -10;
   if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + local_new + n_records)) return -10;
-  if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
-  k_absorb<<<grid_for(n_records, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
-      c->hm.L, c->d_inbox, n_records, c->d_slots, c->log2, c->d_states + d, c->d_parents + d, c->cap - d, c->d_ctr);
-  if (hipGetLastError() != hipSuccess) return -10;
-  if (hipEventRecord(c->e1, c->stream) != hipSuccess) return -10;
-  if (!read_ctr(c)) return -10;
-  float ms = 0;
-  hipEventElapsedTime(&ms, c->e0, c->e1);
-  c->kernel_ms += ms;
-  if (c->h_ctr->overflow) {
-    c->err = "absorb overflowed its FPSet / store; size them up front (opts)";
-    return -11;
+  for (;;) {
+    if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
+    k_absorb<<<grid_for(n_records, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
+        c->hm.L, c->d_inbox, n_records, c->d_slots, c->log2, c->d_states + d, c->d_parents + d, c->cap - d,
+        c->d_ctr);
+    if (hipGetLastError() != hipSuccess) return -10;
+    if (hipEventRecord(c->e1, c->stream) != hipSuccess) return -10;
+    if (!read_ctr(c)) return -10;
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->e0, c->e1);
+    c->kernel_ms += ms;
+    const unsigned ovf = c->h_ctr->overflow;
+    if (!ovf) break;
+    // grow and redo: forget this absorb's appends and inserts
+    ++c->levels_redone;
+    if ((ovf & OVF_STORE) && !ensure_store(c, d + local_new + n_records)) return -10;
+    if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d + local_new)) return -10;
+    *c->h_ctr = before;
+    if (hipMemcpyAsync(c->d_ctr, c->h_ctr, sizeof(LevelCtr), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+      return -10;
   }
+  c->pending = c->h_ctr->n_new;
   fill_stats(c, st);
   return 0;
 }

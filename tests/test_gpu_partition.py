@@ -44,7 +44,9 @@ def run_virtual(model, world, partition=0):
         lv = [sum(x) for x in zip(*[e.level_sizes() for e in engines])]
         while lv and lv[-1] == 0:
             lv.pop()
-        return gen, distinct, lv, max(s.status for s in stats)
+        # open partition: the ranks stay "running"; the driver ends the run
+        st = max(s.status for s in stats)
+        return gen, distinct, lv, st if st >= 2 else 1
     finally:
         for e in engines:
             e.close()
