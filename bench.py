@@ -33,6 +33,28 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_STATE_WORD = 8
 
 
+PMC_PROFILE = "profiles/r01_pmc_k_expand.json"
+MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
+
+
+def load_profile(rel):
+    p = os.path.join(ROOT, rel)
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+def load_microbench(rel):
+    """Best measured rate per access kind (accesses/s) from the microbenchmark log."""
+    p = os.path.join(ROOT, rel)
+    if not os.path.exists(p):
+        return None
+    best = {}
+    for line in open(p):
+        if line.startswith("{"):
+            r = json.loads(line)
+            best[r["kind"]] = max(best.get(r["kind"], 0.0), r["access_per_s"])
+    return best
+
+
 def model_for(cfg):
     import tlcgpu
     k = CONFIGS[cfg]["keys"]
@@ -163,11 +185,29 @@ def main():
     bytes_step = algorithmic_bytes(distinct, generated, n_init, selfloops) / world  # per rank
     expand_ms_step = expand_ms / args.steps
     achieved = bytes_step / (expand_ms_step * 1e-3) / 1e9
+    avg_launch_s = expand_ms_step / launches * 1e-3
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
                     kernel="k_expand", launches_per_step=launches,
                     avg_launch_ms=round(expand_ms_step / launches, 4),
                     bytes_per_distinct=round(algorithmic_bytes(distinct, generated, n_init, selfloops) / distinct, 2))
+    pmc = load_profile(PMC_PROFILE)
+    if pmc and args.config == "g9" and world == 1:
+        # HBM bytes booked by FETCH_SIZE + WRITE_SIZE for k_expand (scripts/pmc.sh, calibrated)
+        roofline["traffic"] = round(pmc["hbm_bytes_per_launch"] / avg_launch_s / 1e9, 1)
+        roofline["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_launch"])
+        roofline["traffic_source"] = PMC_PROFILE
+    micro = load_microbench(MICRO_PROFILE)
+    if micro:
+        # the kernel's real ceiling: scattered 8-B FPSet probes and inserts at the
+        # rates measured on a 16 GiB table (pulsar-tlaplus_amd/bin/fpset_microbench)
+        probes = (generated - n_init - selfloops) / world
+        inserts = (distinct - n_init) / world
+        bound_ms = (probes / micro["load_nt"] + inserts / micro["cas_new"]) * 1e3
+        roofline["scattered_access_roofline"] = dict(
+            probes_per_step=int(probes), inserts_per_step=int(inserts),
+            load_per_s=micro["load_nt"], cas_per_s=micro["cas_new"], bound_ms_per_step=round(bound_ms, 2),
+            frac=round(bound_ms / expand_ms_step, 3), source=MICRO_PROFILE)
     line = {
         "metric": "distinct states/sec, compaction.tla scaled cfg, 1/2/4/8 MI355X vs host TLC",
         "value": round(value, 1),

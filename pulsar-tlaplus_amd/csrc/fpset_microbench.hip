@@ -1,0 +1,94 @@
+// pulsar-tlaplus_amd/csrc/fpset_microbench.hip -- measured ceilings for the
+// FPSet roofline: scattered 8-byte accesses over a table the size of the G9
+// FPSet (2^31 slots = 16 GiB), one independent random slot per lane.
+//   load      plain 8-B load                  (a probe that finds its slot)
+//   load_nt   nontemporal 8-B load
+//   store     plain 8-B store                 (an uncontended insert)
+//   cas_new   atomicCAS(0 -> key) that wins   (an insert)
+//   cas_old   atomicCAS on an occupied slot   (a probe that finds a duplicate)
+//   add       no-return 64-bit atomicAdd
+// Prints one JSON line per access kind: accesses/s and GB/s of touched 8-B words.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+#define CHK(x)                                                                   \
+  do {                                                                           \
+    hipError_t e_ = (x);                                                         \
+    if (e_ != hipSuccess) {                                                      \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));               \
+      std::exit(1);                                                              \
+    }                                                                            \
+  } while (0)
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ u64 mix(u64 x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_access(u64* __restrict__ t, int log2, u64 n, u64 seed, u64* sink) {
+  const int sh = 64 - log2;
+  u64 acc = 0;
+  for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) {
+    const u64 h = mix(i ^ seed);
+    const u64 s = h >> sh;
+    if (KIND == 0) acc += t[s];
+    else if (KIND == 1) acc += __builtin_nontemporal_load(&t[s]);
+    else if (KIND == 2) t[s] = h | 1;
+    else if (KIND == 3) acc += atomicCAS(&t[s], 0ull, h | 1);
+    else if (KIND == 4) acc += atomicCAS(&t[s], 0ull, h | 1);
+    else atomicAdd(&t[s], 1ull);
+  }
+  if (acc == 0x123456789ull) *sink = acc;
+}
+
+int main(int argc, char** argv) {
+  int log2 = argc > 1 ? std::atoi(argv[1]) : 31;
+  u64 n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1ull << 30);
+  u64* t;
+  u64* sink;
+  CHK(hipMalloc(&t, 8ull << log2));
+  CHK(hipMalloc(&sink, 8));
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  const char* names[] = {"load", "load_nt", "store", "cas_new", "cas_old", "add"};
+  for (int grid : {4096, 16384}) {
+    for (int kind = 0; kind < 6; ++kind) {
+      // cas_new wants empty slots at the probed positions, the others do not care
+      CHK(hipMemset(t, 0, 8ull << log2));
+      if (kind == 4) {  // pre-fill the slots cas_old will hit
+        k_access<2><<<grid, 256>>>(t, log2, n, 7, sink);
+      }
+      CHK(hipDeviceSynchronize());
+      CHK(hipEventRecord(a));
+      switch (kind) {
+        case 0: k_access<0><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        case 1: k_access<1><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        case 2: k_access<2><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        case 3: k_access<3><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        case 4: k_access<4><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        default: k_access<5><<<grid, 256>>>(t, log2, n, 7, sink); break;
+      }
+      CHK(hipEventRecord(b));
+      CHK(hipEventSynchronize(b));
+      float ms = 0;
+      CHK(hipEventElapsedTime(&ms, a, b));
+      double rate = (double)n / (ms * 1e-3);
+      std::printf("{\"kind\": \"%s\", \"grid\": %d, \"table_gib\": %.1f, \"accesses\": %llu, \"ms\": %.3f, "
+                  "\"access_per_s\": %.4g, \"word_GBps\": %.1f, \"line64_GBps\": %.1f}\n",
+                  names[kind], grid, (8ull << log2) / 1073741824.0, n, ms, rate, rate * 8 / 1e9,
+                  rate * 64 / 1e9);
+      std::fflush(stdout);
+    }
+  }
+  CHK(hipFree(t));
+  return 0;
+}

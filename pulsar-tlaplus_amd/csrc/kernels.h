@@ -60,6 +60,23 @@ __device__ __forceinline__ int fpset_put(u64* __restrict__ slots, int log2, u64 
   return -1;
 }
 
+// continue an insert from slot i (the slots before it on the probe path are
+// held by other states)
+__device__ __forceinline__ int fpset_put_from(u64* __restrict__ slots, u64 mask, u64 key, u64 i, u64* slot_out) {
+#pragma unroll 1
+  for (int p = 0; p < MAX_PROBE; ++p) {
+    u64 v = __builtin_nontemporal_load(&slots[i]);
+    if (v == key) { *slot_out = i; return 0; }
+    if (v == 0) {
+      u64 old = atomicCAS((unsigned long long*)&slots[i], 0ull, (unsigned long long)key);
+      if (old == 0) { *slot_out = i; return 1; }
+      if (old == key) { *slot_out = i; return 0; }
+    }
+    i = (i + 1) & mask;
+  }
+  return -1;
+}
+
 __device__ __forceinline__ u64 lanemask_lt() {
   const int lane = __lane_id();
   return lane ? (~0ull >> (64 - lane)) : 0ull;

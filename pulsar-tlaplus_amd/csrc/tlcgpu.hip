@@ -232,6 +232,124 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
   if (ev != NO_EVENT) atomicMin(&a.ctr->event, ev);
 }
 
+
+// ---- the fast path of one BFS level (no Producer, discovery order not kept,
+// successors stay on this rank): every thread takes IT parents, derives all
+// their candidate successors first, then issues the FPSet probes of all of
+// them together (2*IT independent loads / CASes in flight per lane) before
+// staging the new ones.  PROBE 0: load, CAS only on an empty slot; PROBE 1:
+// CAS straight away (one round trip, an atomic on every probe).
+template <int IT, int PROBE>
+__global__ __launch_bounds__(BLOCK) void k_expand_fast(ExpandArgs a) {
+  constexpr int NC = 2 * IT;
+  constexpr int CAP = BLOCK * NC;
+  __shared__ u64 s_st[CAP];
+  __shared__ u64 s_par[CAP];
+  __shared__ unsigned s_cnt;
+  __shared__ unsigned long long s_base;
+  const Layout& L = a.L;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  u64 gen = 0;
+  unsigned long long ev = NO_EVENT;
+  const u64 per_chunk = (u64)BLOCK * IT;
+  const u64 ord_last = (1ull << L.ord_bits) - 1;
+  const int sh = 64 - a.log2;
+  const u64 mask = (1ull << a.log2) - 1;
+  const int ord_crash = ordinal_of(L, ACT_CRASH, 0);
+  for (u64 c0 = (u64)blockIdx.x * per_chunk; c0 < a.n_front; c0 += (u64)gridDim.x * per_chunk) {
+    u64 s[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const u64 pi = c0 + (u64)it * BLOCK + threadIdx.x;
+      s[it] = pi < a.n_front ? a.frontier[pi] : 0;
+    }
+    u64 cand[NC], dk[NC], pos[NC], v[NC];
+    bool has[NC];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const u64 pi = c0 + (u64)it * BLOCK + threadIdx.x;
+      const bool valid = pi < a.n_front;
+      const u64 dk0 = (a.front_gidx0 + pi) << L.ord_bits;
+      u64 t = 0;
+      int act = 0;
+      const int r = valid ? compactor_step(L, s[it], &t, &act) : 0;
+      if (r == 2) ev = min(ev, (unsigned long long)make_event(dk0 | (u64)ordinal_of(L, act, 0), EVK_ACTION_ERROR, act));
+      cand[2 * it] = t;
+      has[2 * it] = r == 1;
+      dk[2 * it] = dk0 | (u64)ordinal_of(L, act, 0);
+      u64 t2 = 0;
+      has[2 * it + 1] = valid && crash_step(L, s[it], &t2);
+      cand[2 * it + 1] = t2;
+      dk[2 * it + 1] = dk0 | (u64)ord_crash;
+      int nsucc = (int)has[2 * it] + (int)has[2 * it + 1] + (valid ? selfloop_count(L, s[it]) : 0);
+      gen += (u64)nsucc;
+      if (valid && nsucc == 0 && L.check_deadlock)
+        ev = min(ev, (unsigned long long)make_event(dk0 | ord_last, EVK_DEADLOCK, 0));
+    }
+    // first probe of every candidate, all in flight together
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pos[c] = mix64(cand[c]) >> sh;
+    // after this, v[c] == 0 means "inserted by this lane" (CAS returned 0);
+    // v[c] == key means present; anything else: the slot holds another state
+    if (PROBE == 0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) v[c] = has[c] ? __builtin_nontemporal_load(&a.slots[pos[c]]) : 1;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (has[c] && v[c] == 0)
+          v[c] = atomicCAS((unsigned long long*)&a.slots[pos[c]], 0ull, (unsigned long long)(cand[c] | SLOT_TAG));
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        v[c] = has[c] ? atomicCAS((unsigned long long*)&a.slots[pos[c]], 0ull, (unsigned long long)(cand[c] | SLOT_TAG))
+                      : 1;
+    }
+    // resolve: new / seen; probe on past slots held by other states
+    bool isnew[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      isnew[c] = false;
+      if (!has[c]) continue;
+      const u64 key = cand[c] | SLOT_TAG;
+      if (v[c] == 0) { isnew[c] = true; continue; }
+      if (v[c] == key) continue;
+      u64 slot;
+      const int r = fpset_put_from(a.slots, mask, key, (pos[c] + 1) & mask, &slot);
+      if (r < 0) atomicOr(&a.ctr->overflow, (unsigned)OVF_FPSET);
+      isnew[c] = r == 1;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (isnew[c]) {
+        const int q = check_invariants(L, cand[c]);
+        if (q >= 0) ev = min(ev, (unsigned long long)make_event(dk[c], (q & 1) ? EVK_INV_ERROR : EVK_VIOLATION, q >> 1));
+      }
+      stage_append<false>(isnew[c], cand[c], a.rank_tag | dk[c], 0, s_st, s_par, nullptr, &s_cnt);
+    }
+    // flush the stage: one global atomic per block chunk
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&a.ctr->n_new, (unsigned long long)s_cnt) : 0;
+    __syncthreads();
+    const unsigned n = s_cnt;
+    const u64 b = s_base;
+    if (b + n <= a.cap_out) {
+      for (unsigned i = threadIdx.x; i < n; i += BLOCK) {
+        a.states_out[b + i] = s_st[i];
+        a.parents_out[b + i] = s_par[i];
+      }
+    } else if (threadIdx.x == 0 && n) {
+      atomicOr(&a.ctr->overflow, (unsigned)OVF_STORE);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  }
+  gen = wave_sum_u64(gen);
+  if (__lane_id() == 0 && gen) atomicAdd(&a.ctr->generated, (unsigned long long)gen);
+  if (ev != NO_EVENT) atomicMin(&a.ctr->event, ev);
+}
+
 // ---- TLC order: gather each new state's minimal discovery key
 __global__ __launch_bounds__(BLOCK) void k_gather_dkey(u64 n, const u64* __restrict__ slot_new,
                                                        const u64* __restrict__ dkey_slot, u64* __restrict__ dk) {
@@ -344,6 +462,10 @@ struct tlcg_ctx {
   u64* d_inbox = nullptr;
   u64 inbox_cap = 0;
   u64 pending = 0;      // states appended to the current level, not yet committed
+  // kernel variant (tuning; env TLCG_FAST_ITEMS / TLCG_PROBE / TLCG_GRID)
+  int fast_items = 2;   // parents per thread in k_expand_fast (0 = general kernel)
+  int probe_mode = 0;   // 0 load-then-CAS, 1 CAS-only
+  unsigned grid_cap = 8192;
   bool closed = false;  // partition by immutable `messages`: successors never leave the rank
   // counters
   LevelCtr* d_ctr = nullptr;
@@ -667,8 +789,23 @@ bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
   a.outbox = c->d_outbox;
   a.outbox_cap = c->outbox_cap;
   const bool prod = L.producer != 0, tlc = c->opts.tlc_order != 0;
+  if (!prod && !tlc && !part && c->fast_items > 0) {
+    const int it = c->fast_items;
+    const unsigned g = grid_for(n_front, (u64)BLOCK * it, c->grid_cap);
+    if (c->probe_mode == 0) {
+      if (it == 1) k_expand_fast<1, 0><<<g, BLOCK, 0, c->stream>>>(a);
+      else if (it == 2) k_expand_fast<2, 0><<<g, BLOCK, 0, c->stream>>>(a);
+      else k_expand_fast<4, 0><<<g, BLOCK, 0, c->stream>>>(a);
+    } else {
+      if (it == 1) k_expand_fast<1, 1><<<g, BLOCK, 0, c->stream>>>(a);
+      else if (it == 2) k_expand_fast<2, 1><<<g, BLOCK, 0, c->stream>>>(a);
+      else k_expand_fast<4, 1><<<g, BLOCK, 0, c->stream>>>(a);
+    }
+    HIPCHK(hipGetLastError());
+    return true;
+  }
   const u64 per_block = (u64)BLOCK * (prod ? 1 : ITEMS);
-  const unsigned grid = grid_for(n_front, per_block, 8192);
+  const unsigned grid = grid_for(n_front, per_block, c->grid_cap);
   if (prod) {
     if (tlc) launch_expand_t<true, true, false>(a, grid, c->stream);
     else if (part) launch_expand_t<true, false, true>(a, grid, c->stream);
@@ -798,6 +935,10 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
   c->owner_mask = part == 1 ? c->hm.L.msgs_mask : ~0ull;
   c->closed = c->opts.world == 1 || (part == 1 && !c->hm.L.producer);
   *out = c;
+  if (const char* v = getenv("TLCG_FAST_ITEMS")) c->fast_items = atoi(v);
+  if (const char* v = getenv("TLCG_PROBE")) c->probe_mode = atoi(v);
+  if (const char* v = getenv("TLCG_GRID")) c->grid_cap = (unsigned)atoi(v);
+  if (c->fast_items != 0 && c->fast_items != 1 && c->fast_items != 2 && c->fast_items != 4) c->fast_items = 2;
   hipError_t e = hipSetDevice(c->opts.device);
   if (e != hipSuccess) {
     c->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
