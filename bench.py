@@ -112,6 +112,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="g9", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, one GPU per rank) or gloo (rehearsal)")
     args = ap.parse_args()
 
     import torch
@@ -121,11 +122,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    ndev = torch.cuda.device_count()
+    gpu = local_rank % max(ndev, 1)  # = local_rank on a node with one GPU per rank
     if distributed:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    dev = torch.device(f"cuda:{local_rank}")
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        else:
+            dist.init_process_group(args.dist_backend)
+    dev = torch.device(f"cuda:{gpu}")
+    rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # reduction tensors
 
     cfg = CONFIGS[args.config]
     model = model_for(args.config)
@@ -133,7 +140,7 @@ def main():
     log2 = max(16, (2 * per_rank - 1).bit_length())
     cap = int(per_rank * 1.08) + 2 * (cfg["distinct"] // 12) // world + (1 << 20)
     import dist as tdist
-    eng = tdist.GpuEngine(model, rank, world, local_rank, log2_fpset_slots=log2, state_capacity=cap)
+    eng = tdist.GpuEngine(model, rank, world, gpu, log2_fpset_slots=log2, state_capacity=cap)
     assert eng.closed
 
     def step():
@@ -160,13 +167,13 @@ def main():
     launches = len(levels)  # one expand launch per level (the last finds nothing new)
     local = [st.generated, st.distinct]
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor(local, dtype=torch.int64, device=dev)
+        c = torch.tensor(local, dtype=torch.int64, device=rdev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         local = [int(x) for x in c.tolist()]
-        e = torch.tensor([expand_ms, kernel_ms], dtype=torch.float64, device=dev)
+        e = torch.tensor([expand_ms, kernel_ms], dtype=torch.float64, device=rdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         expand_ms, kernel_ms = [float(x) for x in e.tolist()]
     generated, distinct = local

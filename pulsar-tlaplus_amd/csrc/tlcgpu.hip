@@ -465,7 +465,7 @@ struct tlcg_ctx {
   // kernel variant (tuning; env TLCG_FAST_ITEMS / TLCG_PROBE / TLCG_GRID)
   int fast_items = 2;   // parents per thread in k_expand_fast (0 = general kernel)
   int probe_mode = 0;   // 0 load-then-CAS, 1 CAS-only
-  unsigned grid_cap = 8192;
+  unsigned grid_cap = 16384;
   bool closed = false;  // partition by immutable `messages`: successors never leave the rank
   // counters
   LevelCtr* d_ctr = nullptr;
