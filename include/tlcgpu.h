@@ -99,8 +99,16 @@ typedef struct tlcg_opts {
   int32_t tlc_order;         /* 1: order every level like TLC -workers 1 (exact TLC trace) */
   int32_t rank, world;       /* fingerprint partition: this context owns rank of world */
   int32_t partition;         /* 0 auto (by `messages` when it is immutable), 1 by `messages`, 2 whole state */
-  int32_t reserved[7];
+  int32_t engine;            /* TLCG_ENGINE_*: 0 auto, 1 global HBM FPSet, 2 component (closed partitions) */
+  int32_t reserved[6];
 } tlcg_opts;
+
+/* BFS engines.  GLOBAL: level-synchronous BFS over one HBM FPSet (64-bit CAS),
+ * any model.  COMPONENT: when `messages` is immutable (no Producer) every
+ * initial message sequence spans an independent component; a wavefront lane
+ * runs TLC's FIFO BFS on one component with an on-chip FPSet.  Same counts,
+ * same TLC-order trace; used by AUTO when every component fits on chip. */
+enum { TLCG_ENGINE_AUTO = 0, TLCG_ENGINE_GLOBAL = 1, TLCG_ENGINE_COMPONENT = 2 };
 
 typedef struct tlcg_stats {
   uint64_t generated;        /* "states generated" (initial states included) */
@@ -116,7 +124,8 @@ typedef struct tlcg_stats {
   double kernel_ms;          /* total device time of the BFS kernels so far (HIP events) */
   double expand_ms;          /* device time of the expand kernels alone */
   uint64_t levels_redone;    /* levels re-run after an FPSet / store growth */
-  uint64_t reserved[4];
+  uint64_t engine;           /* TLCG_ENGINE_* that produced these numbers */
+  uint64_t reserved[3];
 } tlcg_stats;
 
 typedef struct tlcg_ctx tlcg_ctx;

@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "component.h"
 #include "host_model.h"
 #include "kernels.h"
 #include "tlcgpu.h"
@@ -461,6 +462,21 @@ struct tlcg_ctx {
   u64 outbox_cap = 0;  // records per destination
   u64* d_inbox = nullptr;
   u64 inbox_cap = 0;
+  // engine of the current run (TLCG_ENGINE_GLOBAL or _COMPONENT)
+  int engine = TLCG_ENGINE_GLOBAL;
+  // component engine: results, scratch, and where each pass put its components
+  struct CompPass {
+    int K;
+    u64 store_base, r0, n;
+    std::vector<u64> list;  // initial-state indices (cascade passes); empty: range [r0, r0 + n)
+  };
+  std::vector<CompPass> passes;
+  std::vector<u64> comp_levels;
+  u64 comp_generated = 0, comp_distinct = 0, comp_store_used = 0;
+  unsigned long long* d_comp = nullptr;  // lvl[COMP_MAXLV], totals[2], event, ovf_n
+  unsigned long long* h_comp = nullptr;
+  u64* d_ovf[2] = {nullptr, nullptr};
+  u64 ovf_cap = 0;
   u64 pending = 0;      // states appended to the current level, not yet committed
   // kernel variant (tuning; env TLCG_FAST_ITEMS / TLCG_PROBE / TLCG_GRID)
   int fast_items = 2;   // parents per thread in k_expand_fast (0 = general kernel)
@@ -501,6 +517,10 @@ namespace {
   } while (0)
 
 u64 distinct_of(const tlcg_ctx* c) { return c->level_base.empty() ? 0 : c->level_base.back(); }
+// first unused slot of the state store
+u64 store_end(const tlcg_ctx* c) {
+  return c->engine == TLCG_ENGINE_COMPONENT ? c->comp_store_used : distinct_of(c);
+}
 
 bool alloc_bytes(tlcg_ctx* c, void** p, size_t bytes, const char* what) {
   hipError_t e = hipMalloc(p, bytes);
@@ -528,7 +548,7 @@ bool ensure_store(tlcg_ctx* c, u64 need) {
   u64 *ns = nullptr, *np = nullptr;
   if (!alloc_bytes(c, (void**)&ns, ncap * 8, "state store")) return false;
   if (!alloc_bytes(c, (void**)&np, ncap * 8, "parent log")) { hipFree(ns); return false; }
-  const u64 keep = std::min<u64>(c->cap, distinct_of(c) + c->pending);
+  const u64 keep = std::min<u64>(c->cap, store_end(c) + c->pending);
   if (keep) {
     HIPCHK(hipMemcpyAsync(ns, c->d_states, keep * 8, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(np, c->d_parents, keep * 8, hipMemcpyDeviceToDevice, c->stream));
@@ -615,12 +635,16 @@ bool read_ctr(tlcg_ctx* c) {
 void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   if (!st) return;
   std::memset(st, 0, sizeof *st);
-  const u64 d = distinct_of(c);
-  const int depth = c->level_base.empty() ? 0 : (int)c->level_base.size() - 1;
-  st->generated = c->generated;
+  const bool comp = c->engine == TLCG_ENGINE_COMPONENT;
+  const u64 d = comp ? c->comp_distinct : distinct_of(c);
+  const int depth = comp ? (int)c->comp_levels.size()
+                         : (c->level_base.empty() ? 0 : (int)c->level_base.size() - 1);
+  st->generated = comp ? c->comp_generated : c->generated;
   st->distinct = d;
-  st->frontier = depth ? c->level_base[(size_t)depth] - c->level_base[(size_t)depth - 1] : 0;
+  st->frontier = comp ? (depth ? c->comp_levels[(size_t)depth - 1] : 0)
+                      : (depth ? c->level_base[(size_t)depth] - c->level_base[(size_t)depth - 1] : 0);
   st->depth = depth;
+  st->engine = (uint64_t)c->engine;
   st->status = c->status;
   st->invariant = -1;
   st->action = -1;
@@ -630,7 +654,7 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
     if (kind == EVK_VIOLATION || kind == EVK_INV_ERROR) st->invariant = (int)(c->ev_word & 15);
     st->action = c->ev_action;
   }
-  const double g = (double)c->generated, n = (double)d;
+  const double g = (double)st->generated, n = (double)d;
   st->fp_collision_optimistic = n * (g - n) / 18446744073709551616.0;
   st->kernel_ms = c->kernel_ms;
   st->expand_ms = c->expand_ms;
@@ -697,7 +721,172 @@ bool resolve_event(tlcg_ctx* c, u64 ev, int level) {
   return true;
 }
 
+
+// Locate a component-engine event (component.h's key) in the store.
+bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
+  const Layout& L = c->hm.L;
+  const int level = (int)(ev >> 56);
+  const u64 idx0 = (ev >> 20) & ((1ull << 36) - 1);
+  const int pos = (int)((ev >> 12) & 255);
+  const int action = (int)((ev >> 8) & 15);
+  const int kind = (int)((ev >> 4) & 3);
+  c->ev_word = ev;
+  c->ev_level = level;
+  switch (kind) {
+    case EVK_VIOLATION: c->status = TLCG_VIOLATION; break;
+    case EVK_INV_ERROR: c->status = TLCG_INVARIANT_ERROR; break;
+    case EVK_DEADLOCK: c->status = TLCG_DEADLOCK; break;
+    default: c->status = TLCG_ACTION_ERROR; break;
+  }
+  if (level == 0) {  // an initial state
+    c->ev_state = init_state(L, idx0);
+    c->ev_parent_gidx = NO_PARENT;
+    c->ev_action = TLCG_ACT_INIT;
+    return true;
+  }
+  // which pass completed this component, and its slot there
+  u64 gidx = NO_PARENT;
+  for (const auto& ps : c->passes) {
+    u64 ci = NO_PARENT;
+    if (ps.list.empty()) {
+      if (idx0 >= ps.r0 && idx0 < ps.r0 + ps.n) ci = idx0 - ps.r0;
+    } else {
+      for (u64 i = 0; i < ps.list.size(); ++i)
+        if (ps.list[i] == idx0) ci = i;
+    }
+    if (ci != NO_PARENT) gidx = ps.store_base + (ci / 64) * (u64)ps.K * 64 + (u64)pos * 64 + (ci % 64);
+  }
+  if (gidx == NO_PARENT) {
+    c->err = "internal: component of the event not found";
+    return false;
+  }
+  u64 ps = 0, pp = 0;
+  if (!state_at(c, gidx, &ps, &pp)) return false;
+  c->ev_parent_gidx = gidx;
+  c->ev_parent_ref = ((u64)c->opts.rank << 56) | (gidx << L.ord_bits);
+  if (kind == EVK_DEADLOCK) {
+    c->ev_state = ps;
+    c->ev_action = -1;
+  } else if (kind == EVK_ACTION_ERROR) {
+    c->ev_state = ps;
+    c->ev_action = action;
+  } else {
+    u64 t = 0;
+    if (successor_at(L, ps, ordinal_of(L, action, 0), &t) != 1) {
+      c->err = "internal: violating successor could not be re-derived";
+      return false;
+    }
+    c->ev_state = t;
+    c->ev_action = action;
+  }
+  return true;
+}
+
+// ---- component engine (component.h) ----
+
+// applicable: `messages` immutable, one rank's components all local, local key fits 32 bits
+bool component_applicable(const tlcg_ctx* c) {
+  const Layout& L = c->hm.L;
+  const int mb = L.msg_sh + L.N * L.mw;
+  return !L.producer && !c->opts.tlc_order && c->closed && L.bits - mb <= 32 && c->hm.n_init < (1ull << 36);
+}
+
+bool comp_scratch(tlcg_ctx* c, u64 n) {
+  if (!c->d_comp) {
+    const size_t bytes = sizeof(unsigned long long) * (COMP_MAXLV + 4);
+    if (!alloc_bytes(c, (void**)&c->d_comp, bytes, "component counters")) return false;
+    HIPCHK(hipHostMalloc((void**)&c->h_comp, bytes));
+  }
+  if (n > c->ovf_cap) {
+    hipFree(c->d_ovf[0]);
+    hipFree(c->d_ovf[1]);
+    c->d_ovf[0] = c->d_ovf[1] = nullptr;
+    c->ovf_cap = 0;
+    if (!alloc_bytes(c, (void**)&c->d_ovf[0], n * 8, "overflow list")) return false;
+    if (!alloc_bytes(c, (void**)&c->d_ovf[1], n * 8, "overflow list")) return false;
+    c->ovf_cap = n;
+  }
+  return true;
+}
+
+// Run every component of this rank on chip: K = 64, then the overflow at
+// K = 128, then 255.  Returns 1 done, 0 some component does not fit (caller
+// falls back to the global engine), -1 error.
+int run_component(tlcg_ctx* c) {
+  const HostModel& hm = c->hm;
+  const Layout& L = hm.L;
+  const int mb = L.msg_sh + L.N * L.mw;
+  const u64 W = (u64)c->opts.world, R = (u64)c->opts.rank;
+  const u64 r0 = hm.n_init * R / W, r1 = hm.n_init * (R + 1) / W;
+  c->engine = TLCG_ENGINE_COMPONENT;
+  c->passes.clear();
+  c->comp_levels.assign(COMP_MAXLV, 0);
+  c->comp_generated = c->comp_distinct = c->comp_store_used = 0;
+  c->pending = 0;
+  if (!comp_scratch(c, std::max<u64>(r1 - r0, 1))) return -1;
+  static const int kCascade[3] = {64, 128, 255};
+  u64 n = r1 - r0;
+  int cur = -1;  // overflow list holding this pass's components (-1: range)
+  u64 best_ev = NO_EVENT;
+  for (int p = 0; p < 3 && n; ++p) {
+    const int K = kCascade[p];
+    const u64 base = c->comp_store_used;
+    const u64 slots = component_store_slots(n, K);
+    if (!ensure_store(c, base + slots)) return -1;
+    tlcg_ctx::CompPass pass{K, base, r0, n, {}};
+    if (cur >= 0) {
+      pass.list.resize(n);
+      HIPCHK(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
+    }
+    const int out = cur == 0 ? 1 : 0;
+    HIPCHK(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * (COMP_MAXLV + 4), c->stream));
+    HIPCHK(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
+    CompArgs a;
+    a.L = L;
+    a.comp0 = r0;
+    a.n_comp = n;
+    a.list = cur >= 0 ? c->d_ovf[cur] : nullptr;
+    a.store = c->d_states + base;
+    a.parents = c->d_parents + base;
+    a.store_base = base;
+    a.msgs_bits = mb;
+    a.rank_tag = (u64)c->opts.rank << 56;
+    a.lvl = c->d_comp;
+    a.totals = c->d_comp + COMP_MAXLV;
+    a.event = c->d_comp + COMP_MAXLV + 2;
+    a.ovf_n = c->d_comp + COMP_MAXLV + 3;
+    a.ovf_list = c->d_ovf[out];
+    HIPCHK(hipEventRecord(c->e0, c->stream));
+    if (!launch_component(a, K, c->stream)) {
+      c->err = "component kernel launch failed";
+      return -1;
+    }
+    HIPCHK(hipEventRecord(c->e1, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * (COMP_MAXLV + 4),
+                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->e0, c->e1);
+    c->kernel_ms += ms;
+    c->expand_ms += ms;
+    for (int l = 0; l < COMP_MAXLV; ++l) c->comp_levels[(size_t)l] += c->h_comp[l];
+    c->comp_generated += c->h_comp[COMP_MAXLV];
+    c->comp_distinct += c->h_comp[COMP_MAXLV + 1];
+    best_ev = std::min<u64>(best_ev, c->h_comp[COMP_MAXLV + 2]);
+    c->comp_store_used = base + slots;
+    c->passes.push_back(std::move(pass));
+    n = c->h_comp[COMP_MAXLV + 3];
+    cur = out;
+  }
+  if (n) return 0;  // components beyond 255 states / 48 levels: the global engine takes the model
+  while (!c->comp_levels.empty() && c->comp_levels.back() == 0) c->comp_levels.pop_back();
+  if (best_ev != NO_EVENT) return resolve_comp_event(c, best_ev) ? 1 : -1;
+  c->status = TLCG_DONE;
+  return 1;
+}
+
 bool run_init(tlcg_ctx* c) {
+  c->engine = TLCG_ENGINE_GLOBAL;
   const HostModel& hm = c->hm;
   const Layout& L = hm.L;
   c->level_base.assign(1, 0);
@@ -934,6 +1123,11 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
   const int part = c->opts.partition ? c->opts.partition : (c->hm.L.producer ? 2 : 1);
   c->owner_mask = part == 1 ? c->hm.L.msgs_mask : ~0ull;
   c->closed = c->opts.world == 1 || (part == 1 && !c->hm.L.producer);
+  if (c->opts.engine == TLCG_ENGINE_COMPONENT && !component_applicable(c)) {
+    c->err = "the component engine needs an immutable `messages` (no Producer), no TLC-order mode and a closed partition";
+    *out = c;
+    return -2;
+  }
   *out = c;
   if (const char* v = getenv("TLCG_FAST_ITEMS")) c->fast_items = atoi(v);
   if (const char* v = getenv("TLCG_PROBE")) c->probe_mode = atoi(v);
@@ -978,6 +1172,10 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_inbox);
   hipFree(c->d_ctr);
   hipFree(c->d_aux);
+  hipFree(c->d_comp);
+  hipFree(c->d_ovf[0]);
+  hipFree(c->d_ovf[1]);
+  if (c->h_comp) hipHostFree(c->h_comp);
   if (c->h_ctr) hipHostFree(c->h_ctr);
   if (c->h_aux) hipHostFree(c->h_aux);
   if (c->e0) hipEventDestroy(c->e0);
@@ -993,6 +1191,26 @@ void* tlcg_stream(tlcg_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
   if (!c || !c->stream) return -1;
+  c->kernel_ms = c->expand_ms = 0;
+  c->status = TLCG_RUNNING;
+  c->ev_word = NO_EVENT;
+  c->ev_level = -1;
+  c->ev_parent_gidx = NO_PARENT;
+  c->ev_action = -1;
+  if (c->opts.engine != TLCG_ENGINE_GLOBAL && component_applicable(c)) {
+    // the component engine runs the whole BFS here; 0 = a component needs the global engine
+    const int r = run_component(c);
+    if (r < 0) return -10;
+    if (r == 1) {
+      c->inited = true;
+      fill_stats(c, st);
+      return 0;
+    }
+    if (c->opts.engine == TLCG_ENGINE_COMPONENT) {
+      c->err = "a component does not fit on chip (over 255 states or 48 levels); use the global engine";
+      return -12;
+    }
+  }
   if (!run_init(c)) return -10;
   c->inited = true;
   fill_stats(c, st);
@@ -1001,6 +1219,10 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
 
 int tlcg_step_level(tlcg_ctx* c, tlcg_stats* st) {
   if (!c || !c->inited) return -1;
+  if (c->engine == TLCG_ENGINE_COMPONENT) {  // the run finished in tlcg_init
+    fill_stats(c, st);
+    return 0;
+  }
   if (!c->closed) {
     c->err = "successors can leave this rank: use tlcg_expand/outbox/inbox/absorb/end_level";
     return -2;
@@ -1023,6 +1245,12 @@ int tlcg_run(tlcg_ctx* c, tlcg_stats* st) {
 
 int tlcg_level_sizes(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
   if (!c) return -1;
+  if (c->engine == TLCG_ENGINE_COMPONENT) {
+    const int depth = (int)c->comp_levels.size();
+    for (int i = 0; i < depth && i < cap; ++i) out[i] = c->comp_levels[(size_t)i];
+    if (n) *n = depth;
+    return 0;
+  }
   const int depth = c->level_base.empty() ? 0 : (int)c->level_base.size() - 1;
   for (int i = 0; i < depth && i < cap; ++i) out[i] = c->level_base[(size_t)i + 1] - c->level_base[(size_t)i];
   if (n) *n = depth;
@@ -1030,7 +1258,7 @@ int tlcg_level_sizes(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
 }
 
 int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref) {
-  if (!c || gidx >= distinct_of(c)) return -1;
+  if (!c || gidx >= store_end(c)) return -1;
   u64 s = 0, p = 0;
   if (!state_at(c, gidx, &s, &p)) return -10;
   if (state) *state = s;
@@ -1039,7 +1267,7 @@ int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_
 }
 
 int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
-  if (!c || first + n > distinct_of(c)) return -1;
+  if (!c || first + n > store_end(c)) return -1;
   if (n && hipMemcpy(out, c->d_states + first, n * 8, hipMemcpyDeviceToHost) != hipSuccess) {
     c->err = "copy failed";
     return -10;

@@ -26,6 +26,7 @@ ACTIONS = ("Producer", "CompactorPhaseOne", "CompactorPhaseTwoWrite", "Compactor
            "CompactorPhaseTwoUpdateHorizon", "CompactorPhaseTwoPersistCusror", "CompactorPhaseTwoDeleteLedger",
            "BrokerCrash", "Consumer", "Terminating")
 STATUS = {0: "running", 1: "ok", 2: "invariant", 3: "deadlock", 4: "action_error", 5: "invariant_error"}
+ENGINES = {"auto": 0, "global": 1, "component": 2}
 
 
 class tlcg_model(C.Structure):
@@ -41,14 +42,15 @@ class tlcg_model(C.Structure):
 class tlcg_opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("log2_fpset_slots", C.c_int32), ("state_capacity", C.c_uint64),
                 ("tlc_order", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32), ("partition", C.c_int32),
-                ("reserved", C.c_int32 * 7)]
+                ("engine", C.c_int32), ("reserved", C.c_int32 * 6)]
 
 
 class tlcg_stats(C.Structure):
     _fields_ = [("generated", C.c_uint64), ("distinct", C.c_uint64), ("frontier", C.c_uint64),
                 ("depth", C.c_int32), ("status", C.c_int32), ("invariant", C.c_int32), ("action", C.c_int32),
                 ("event_gidx", C.c_uint64), ("fp_collision_optimistic", C.c_double), ("kernel_ms", C.c_double),
-                ("expand_ms", C.c_double), ("levels_redone", C.c_uint64), ("reserved", C.c_uint64 * 4)]
+                ("expand_ms", C.c_double), ("levels_redone", C.c_uint64), ("engine", C.c_uint64),
+                ("reserved", C.c_uint64 * 3)]
 
 
 _lib = None
@@ -217,6 +219,7 @@ class Result:
     kernel_ms: float = 0.0
     expand_ms: float = 0.0
     levels_redone: int = 0
+    engine: str = ""
     trace: List[Tuple[str, int]] = field(default_factory=list)
 
 
@@ -224,13 +227,15 @@ class Checker:
     """One checking context on one GPU (libtlcgpu tlcg_ctx)."""
 
     def __init__(self, model: Model, device: int = 0, log2_fpset_slots: int = 0, state_capacity: int = 0,
-                 tlc_order: bool = False, rank: int = 0, world: int = 1, partition: int = 0):
+                 tlc_order: bool = False, rank: int = 0, world: int = 1, partition: int = 0,
+                 engine: str = "auto"):
         self.lib = load_library()
         self.model = model
         self._m = model.to_c()
         o = tlcg_opts()
         o.device, o.log2_fpset_slots, o.state_capacity = device, log2_fpset_slots, state_capacity
         o.tlc_order, o.rank, o.world, o.partition = int(tlc_order), rank, world, partition
+        o.engine = ENGINES[engine]
         self._o = o
         self.ctx = C.c_void_p()
         rc = self.lib.tlcg_create(C.byref(self._m), C.byref(o), C.byref(self.ctx))
@@ -298,7 +303,8 @@ class Checker:
         r = Result(status=status, generated=s.generated, distinct=s.distinct, depth=s.depth,
                    left_on_queue=0 if status == "ok" else s.frontier, levels=self.level_sizes(),
                    collision_optimistic=s.fp_collision_optimistic, kernel_ms=s.kernel_ms,
-                   expand_ms=s.expand_ms, levels_redone=s.levels_redone)
+                   expand_ms=s.expand_ms, levels_redone=s.levels_redone,
+                   engine={v: k for k, v in ENGINES.items()}.get(s.engine, "?"))
         if s.invariant >= 0:
             r.invariant = self.model.invariants[s.invariant]
         if s.action >= 0:

@@ -30,7 +30,7 @@ def check_against_golden(case, r, tlc_order):
     assert len(r.trace) == len(want_trace)
     if want["result"] == "invariant":
         assert r.invariant == want["invariant"]
-    if tlc_order:
+    if tlc_order or r.engine == "component":  # both reproduce TLC's -workers 1 trace
         assert [a for a, _ in r.trace] == [t["action"] for t in want_trace]
         assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want_trace]
     else:
@@ -43,12 +43,23 @@ def check_against_golden(case, r, tlc_order):
             assert c >= 0 and m.invariants[c >> 1] == want["invariant"]
 
 
-@pytest.mark.parametrize("tlc_order", [False, True])
+@pytest.mark.parametrize("mode", ["auto", "global", "tlc_order"])
 @pytest.mark.parametrize("case", FULL_CASES)
-def test_golden_case(case, tlc_order):
+def test_golden_case(case, mode):
     m = model_of(GOLDEN[case]["constants"])
-    r = tlcgpu.run(m, tlc_order=tlc_order)
-    check_against_golden(case, r, tlc_order)
+    r = tlcgpu.run(m, tlc_order=mode == "tlc_order", engine="global" if mode == "global" else "auto")
+    check_against_golden(case, r, mode == "tlc_order")
+    c = GOLDEN[case]["constants"]
+    if mode == "auto" and not c["producer"] and want_ok(case):
+        # components are isomorphic (SURVEY App.A.1): all fit on chip iff one does
+        g = GOLDEN[case]["result"]
+        per_component = g["distinct"] // tlcgpu.init_count(m)
+        fits = per_component <= 255 and g["depth"] <= 47
+        assert r.engine == ("component" if fits else "global"), (r.engine, per_component)
+
+
+def want_ok(case):
+    return GOLDEN[case]["result"]["result"] == "ok"
 
 
 def per_m_law(case_first_m, n_m, r):
@@ -71,7 +82,7 @@ def test_m8_scaled_counts():
 def test_g9_scaled_counts_and_parent_log():
     # ~1e9: KeySpace = ValueSpace = 1..15 -> 16^6 message sequences x 62
     m = tlcgpu.Model(**G9)
-    ck = tlcgpu.Checker(m, log2_fpset_slots=31, state_capacity=1_100_000_000)
+    ck = tlcgpu.Checker(m, log2_fpset_slots=31, state_capacity=1_100_000_000, engine="global")
     try:
         r = ck.run(with_trace=False)
         per_m_law("G9_first_M", 16 ** 6, r)
@@ -144,3 +155,36 @@ def test_tlc_order_levels_are_sorted_by_discovery():
         assert ordbits > 0
     finally:
         ck.close()
+
+
+def test_g9_component_engine():
+    # the component engine on the ~1e9 config: same counts and per-level sizes
+    m = tlcgpu.Model(**G9)
+    ck = tlcgpu.Checker(m, engine="component")
+    try:
+        r = ck.run(with_trace=False)
+        assert r.engine == "component"
+        per_m_law("G9_first_M", 16 ** 6, r)
+        # spot-check the store: component 0 (lane 0 of batch 0) is message sequence M0,
+        # stored FIFO at gidx 64 * position; parents point one level up the chain
+        s0, p0 = ck.state_at(0)
+        assert s0 == tlcgpu.host_init_state(m, 0) and p0 == (1 << 64) - 1
+        s1, p1 = ck.state_at(64)
+        assert ("CompactorPhaseOne", s1) in tlcgpu.host_successors(m, s0)
+    finally:
+        ck.close()
+
+
+def test_component_engine_multi_rank_ranges():
+    m = model_of(GOLDEN["X_keys3_vals57"]["constants"])
+    want = GOLDEN["X_keys3_vals57"]["result"]
+    tot_g = tot_d = 0
+    for rank in range(3):
+        ck = tlcgpu.Checker(m, rank=rank, world=3, engine="component")
+        try:
+            r = ck.run(with_trace=False)
+            tot_g += r.generated
+            tot_d += r.distinct
+        finally:
+            ck.close()
+    assert (tot_g, tot_d) == (want["generated"], want["distinct"])
