@@ -186,6 +186,10 @@ int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records);
 int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st);
 int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st);
 
+/* Diagnostic: compile the kernels specialized for these constants (hipRTC)
+ * for `arch` without a device; returns the code-object size or <0 (err). */
+int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t cap);
+
 /* HIP stream (hipStream_t) the context launches on, for event timing. */
 void* tlcg_stream(tlcg_ctx* c);
 

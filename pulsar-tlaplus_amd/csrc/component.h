@@ -16,10 +16,12 @@
 // the event key (level, component, position, action) orders errors like TLC
 // and the parent chain is TLC's trace.
 #pragma once
+#if !defined(__HIPCC_RTC__)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "model.h"
+#endif
 
 namespace tlcg {
 
@@ -48,10 +50,12 @@ TLCG_HD u64 make_comp_event(int level, u64 comp, int pos, int action, int kind, 
          ((u64)(action & 15) << 8) | ((u64)kind << 4) | (u64)(index & 15);
 }
 
+#if !defined(__HIPCC_RTC__)
 // launches the component BFS with on-chip capacity K states per component
-// (K = 64 or 255); returns false on a launch error
+// (K = 64, 128 or 255); returns false on a launch error
 bool launch_component(const CompArgs& a, int K, hipStream_t stream);
+#endif
 // store slots a launch of n components needs at capacity K
-u64 component_store_slots(u64 n_comp, int K);
+TLCG_HD u64 component_store_slots(u64 n_comp, int K) { return (n_comp + 63) / 64 * (u64)K * 64; }
 
 }  // namespace tlcg

@@ -1,0 +1,162 @@
+// pulsar-tlaplus_amd/csrc/component_body.h -- device body of the component
+// engine (component.h), shared by the precompiled kernel (component.hip) and
+// the run-time specialized one (jit.cpp).
+#pragma once
+#if !defined(__HIPCC_RTC__)
+#include "component.h"
+#include "kernels.h"
+#endif
+
+namespace tlcg {
+
+__device__ __forceinline__ unsigned slot_of(uint32_t key, int log2t) { return (key * 0x9E3779B1u) >> (32 - log2t); }
+
+template <int K>
+struct CompShape;
+template <>
+struct CompShape<64> { static constexpr int LOG2T = 7; };
+template <>
+struct CompShape<128> { static constexpr int LOG2T = 8; };
+template <>
+struct CompShape<255> { static constexpr int LOG2T = 9; };
+
+// the BFS of one wave's components; L is the runtime layout (precompiled
+// kernel) or a constexpr one (jit.cpp), in which case every field folds
+template <int K>
+__device__ __forceinline__ void component_body(const CompArgs& a, const Layout& L) {
+  constexpr int LOG2T = CompShape<K>::LOG2T;
+  constexpr int T = 1 << LOG2T;
+  __shared__ uint32_t q[K][64];                   // FIFO of local keys (word >> msgs_bits)
+  __shared__ uint8_t h[T][64];                    // FPSet: 1 + queue position, 0 = empty
+  __shared__ uint8_t bnd[COMP_MAXLV + 1][64];     // queue position where each level starts
+  __shared__ unsigned lvl_sh[COMP_MAXLV];
+  const int lane = threadIdx.x;
+  const int mb = L.msg_sh + L.N * L.mw;  // `messages` occupies the low mb bits
+  if (lane < COMP_MAXLV) lvl_sh[lane] = 0;
+  u64 gen = 0, dist = 0;
+  unsigned long long ev = NO_EVENT;
+  __syncthreads();
+  for (u64 b = blockIdx.x; b * 64 < a.n_comp; b += gridDim.x) {
+    const u64 ci = b * 64 + (u64)lane;
+    const bool act = ci < a.n_comp;
+    const u64 idx0 = act ? (a.list ? a.list[ci] : a.comp0 + ci) : 0;
+    // clear this wave's FPSet with 16-B stores across the whole [T][64] array
+    for (int i = lane; i < T * 64 / 16; i += 64) reinterpret_cast<uint4*>(&h[0][0])[i] = make_uint4(0, 0, 0, 0);
+    const u64 s0 = init_state(L, idx0);
+    const u64 msgs = s0 & L.msgs_mask;
+    u64* st = a.store + b * (u64)K * 64 + (u64)lane;
+    u64* par = a.parents + b * (u64)K * 64 + (u64)lane;
+    const u64 gbase = a.store_base + b * (u64)K * 64 + (u64)lane;
+    int head = 0, tail = 0, level = 0, lvl_end = 0;
+    bool alive = act, ovf = false;
+    u64 lgen = 0;
+    u64 lev = NO_EVENT;
+    if (act) {
+      const uint32_t k0 = (uint32_t)(s0 >> mb);
+      h[slot_of(k0, LOG2T)][lane] = 1;
+      q[0][lane] = k0;
+      tail = 1;
+      st[0] = s0;
+      par[0] = NO_PARENT;
+      lgen = 1;
+      const int c = check_invariants(L, s0);
+      if (c >= 0) {  // an initial state violates: level field 0 sorts before every expansion
+        lev = make_comp_event(0, idx0, 0, 0, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1);
+        alive = false;
+      }
+    }
+    bnd[0][lane] = 0;
+    lvl_end = tail;
+    // visit one successor: FPSet lookup, insert, invariants (TLC's FPSet.put + check)
+    auto visit = [&](u64 t, int action, int pos) {
+      const uint32_t key = (uint32_t)(t >> mb);
+      unsigned sl = slot_of(key, LOG2T);
+      for (int p = 0; p < T; ++p) {
+        const unsigned e = h[sl][lane];
+        if (e == 0) break;
+        if (q[e - 1][lane] == key) return;  // seen
+        sl = (sl + 1) & (T - 1);
+      }
+      if (tail >= K) {  // does not fit on chip: cascade
+        ovf = true;
+        alive = false;
+        return;
+      }
+      h[sl][lane] = (uint8_t)(tail + 1);
+      q[tail][lane] = key;
+      st[(u64)tail * 64] = t;
+      par[(u64)tail * 64] = a.rank_tag | ((gbase + (u64)pos * 64) << L.ord_bits) | (u64)ordinal_of(L, action, 0);
+      ++tail;
+      const int c = check_invariants(L, t);
+      if (c >= 0) {
+        lev = min(lev, make_comp_event(level + 1, idx0, pos, action, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+        alive = false;
+      }
+    };
+    while (alive && head < tail) {
+      const u64 s = msgs | ((u64)q[head][lane] << mb);
+      int nsucc = 0;
+      u64 t = 0;
+      int action = 0;
+      const int r = compactor_step(L, s, &t, &action);  // compaction.tla:221-226
+      if (r == 2) {
+        lev = min(lev, make_comp_event(level + 1, idx0, head, action, EVK_ACTION_ERROR, action));
+        alive = false;
+        break;
+      }
+      if (r == 1) {
+        ++nsucc;
+        visit(t, action, head);
+      }
+      u64 t2 = 0;
+      if (alive && crash_step(L, s, &t2)) {  // BrokerCrash, compaction.tla:227
+        ++nsucc;
+        visit(t2, ACT_CRASH, head);
+      }
+      nsucc += selfloop_count(L, s);  // Consumer / Terminating stutters
+      lgen += (u64)nsucc;
+      if (alive && nsucc == 0 && L.check_deadlock) {
+        lev = min(lev, make_comp_event(level + 1, idx0, head, 15, EVK_DEADLOCK, 0));
+        alive = false;
+      }
+      if (!alive) break;
+      ++head;
+      if (head == lvl_end) {
+        ++level;
+        if (level >= COMP_MAXLV) {
+          ovf = true;
+          break;
+        }
+        bnd[level][lane] = (uint8_t)head;  // the new level is [head, tail)
+        lvl_end = tail;
+      }
+    }
+    if (act && ovf) {
+      const unsigned long long k = atomicAdd(a.ovf_n, 1ull);
+      a.ovf_list[k] = idx0;
+    } else if (act) {
+      gen += lgen;
+      dist += (u64)tail;
+      ev = min(ev, (unsigned long long)lev);
+      // levels 0..level-1 are complete; `level` is [bnd[level], lvl_end); a lane
+      // stopped by an error also has level+1 partly discovered: [lvl_end, tail)
+      for (int l = 0; l < level; ++l) atomicAdd(&lvl_sh[l], (unsigned)(bnd[l + 1][lane] - bnd[l][lane]));
+      if (level < COMP_MAXLV && lvl_end > bnd[level][lane]) atomicAdd(&lvl_sh[level], (unsigned)(lvl_end - bnd[level][lane]));
+      if (level + 1 < COMP_MAXLV && tail > lvl_end) atomicAdd(&lvl_sh[level + 1], (unsigned)(tail - lvl_end));
+    }
+  }
+  gen = wave_sum_u64(gen);
+  dist = wave_sum_u64(dist);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ev = min(ev, (unsigned long long)__shfl_xor(ev, off));
+  __syncthreads();
+  if (lane == 0) {
+    if (gen) atomicAdd(&a.totals[0], (unsigned long long)gen);
+    if (dist) atomicAdd(&a.totals[1], (unsigned long long)dist);
+    if (ev != NO_EVENT) atomicMin(a.event, ev);
+  }
+  if (lane < COMP_MAXLV && lvl_sh[lane]) atomicAdd(&a.lvl[lane], (unsigned long long)lvl_sh[lane]);
+}
+
+
+}  // namespace tlcg

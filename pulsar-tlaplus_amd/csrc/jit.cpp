@@ -1,0 +1,158 @@
+// pulsar-tlaplus_amd/csrc/jit.cpp -- hipRTC specialization of the component
+// kernel (see jit.h).  The source is the same component_body.h the
+// precompiled kernel uses, plus `constexpr Layout kL = {...}`.
+#include "jit.h"
+
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+#include <vector>
+
+#include "jit_sources.inc"
+
+namespace tlcg {
+
+namespace {
+
+std::string layout_literal(const Layout& L) {
+  std::ostringstream o;
+  o << "constexpr tlcg::Layout kL = {";
+#define F(x) o << "." #x " = " << L.x << ", ";
+  F(N) F(C) F(K) F(ctl) F(nk) F(nv) F(nkv) F(kb) F(vb) F(mw) F(len_sh) F(len_w) F(msg_sh) F(led_sh) F(led_w)
+  F(p1r_sh) F(p1r_w) F(cur_sh) F(curh_w) F(curc_w) F(ph_sh) F(hz_sh) F(hz_w) F(ctx_sh) F(ctx_w) F(cr_sh) F(cr_w)
+  F(bits) F(retain) F(producer) F(consumer) F(term_ok) F(check_deadlock) F(ord_bits) F(n_inv)
+#undef F
+  o << ".inv = {";
+  for (int i = 0; i < 8; ++i) o << L.inv[i] << (i < 7 ? ", " : "");
+  o << "}, .msgs_mask = " << L.msgs_mask << "ull, .led_present_mask = " << L.led_present_mask << "ull};\n";
+  return o.str();
+}
+
+std::string program_source(const Layout& L) {
+  std::string s = "typedef unsigned char uint8_t; typedef unsigned int uint32_t; typedef int int32_t;\n"
+                  "typedef unsigned long uint64_t; typedef long int64_t;\n";
+  s += kJitSource;
+  s += "\n" + layout_literal(L);
+  for (int K : {64, 128, 255})
+    s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_component_" + std::to_string(K) +
+         "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ">(a, kL); }\n";
+  return s;
+}
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) { h ^= c; h *= 1099511628211ull; }
+  return h;
+}
+
+std::string cache_dir() {
+  const char* d = std::getenv("TLCG_JIT_CACHE");
+  return d && *d ? d : "/tmp/tlcgpu-jit";
+}
+
+bool read_all(const std::string& p, std::vector<char>* out) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) return false;
+  out->assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+  return !out->empty();
+}
+
+}  // namespace
+
+bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err) {
+  const std::string src = program_source(L);
+  if (const char* dump = std::getenv("TLCG_JIT_DUMP")) {  // diagnostics: the generated source
+    std::ofstream f(dump);
+    f << src;
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "tlcg_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    *err = "hiprtcCreateProgram failed";
+    return false;
+  }
+  const std::string a = "--offload-arch=" + arch;
+  const char* opts[] = {a.c_str(), "-O3", "-std=c++20"};
+  const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+  if (r != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    hiprtcGetProgramLog(prog, &log[0]);
+    *err = "hipRTC compile failed: " + log.substr(0, 4000);
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  code->resize(n);
+  hiprtcGetCode(prog, code->data());
+  hiprtcDestroyProgram(&prog);
+  if (const char* dump = std::getenv("TLCG_JIT_DUMP")) {
+    std::ofstream f(std::string(dump) + ".co", std::ios::binary);
+    f.write(code->data(), (std::streamsize)code->size());
+  }
+  return true;
+}
+
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    *err = "hipGetDeviceProperties failed";
+    return false;
+  }
+  std::string arch = prop.gcnArchName;
+  arch = arch.substr(0, arch.find(':'));
+  const std::string src = program_source(L);
+  char key[64];
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v1"));
+  const std::string dir = cache_dir();
+  const std::string path = dir + "/" + key + "-" + arch + ".co";
+  std::vector<char> code;
+  out->cached = read_all(path, &code);
+  if (!out->cached) {
+    auto t0 = std::chrono::steady_clock::now();
+    if (!jit_compile(L, arch, &code, err)) return false;
+    out->compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    mkdir(dir.c_str(), 0777);
+    const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+    std::ofstream f(tmp, std::ios::binary);
+    if (f.write(code.data(), (std::streamsize)code.size())) {
+      f.close();
+      std::rename(tmp.c_str(), path.c_str());
+    }
+  }
+  if (hipModuleLoadData(&out->module, code.data()) != hipSuccess) {
+    *err = "hipModuleLoadData failed for the specialized kernels";
+    return false;
+  }
+  const char* names[3] = {"tlcg_component_64", "tlcg_component_128", "tlcg_component_255"};
+  for (int i = 0; i < 3; ++i)
+    if (hipModuleGetFunction(&out->component[i], out->module, names[i]) != hipSuccess) {
+      *err = std::string("hipModuleGetFunction ") + names[i];
+      return false;
+    }
+  return true;
+}
+
+void jit_release(JitKernels* k) {
+  if (k && k->module) hipModuleUnload(k->module);
+  if (k) *k = JitKernels();
+}
+
+bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, hipStream_t stream) {
+  if (!a.n_comp) return true;
+  const int i = K == 64 ? 0 : K == 128 ? 1 : 2;
+  const uint64_t batches = (a.n_comp + 63) / 64;
+  const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
+  CompArgs copy = a;
+  void* args[] = {&copy};
+  return hipModuleLaunchKernel(k.component[i], grid, 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
+}
+
+}  // namespace tlcg

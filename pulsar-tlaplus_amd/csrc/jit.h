@@ -1,0 +1,29 @@
+// pulsar-tlaplus_amd/csrc/jit.h -- run-time specialization of the hot kernels
+// for one model's constants (hipRTC; the layout becomes a constexpr, so every
+// field shift folds and every loop over N / C / invariants unrolls).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "component.h"
+
+namespace tlcg {
+
+struct JitKernels {
+  hipModule_t module = nullptr;
+  hipFunction_t component[3] = {nullptr, nullptr, nullptr};  // K = 64, 128, 255
+  double compile_s = 0;  // 0 when loaded from the cache
+  bool cached = false;
+};
+
+// builds (or loads from $TLCG_JIT_CACHE, default /tmp/tlcgpu-jit) the
+// kernels specialized for L on `device`; false with a message on failure
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err);
+// compile only (no device needed): the code object for `arch`
+bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err);
+void jit_release(JitKernels* k);
+bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, hipStream_t stream);
+
+}  // namespace tlcg

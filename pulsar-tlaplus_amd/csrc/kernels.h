@@ -1,10 +1,12 @@
 // pulsar-tlaplus_amd/csrc/kernels.h -- device-side building blocks of the
 // BFS level: FPSet insert, LDS staging, the per-level counter block.
 #pragma once
+#if !defined(__HIPCC_RTC__)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "model.h"
+#endif
 
 namespace tlcg {
 
@@ -100,6 +102,27 @@ __device__ __forceinline__ void stage_append(bool pred, u64 st, u64 par, u64 slo
     if (WITH_SLOT) s_slot[pos] = slot;
   }
 }
+
+// arguments of one BFS level's expansion (the global engine)
+struct ExpandArgs {
+  Layout L;
+  const u64* frontier;
+  u64 n_front;
+  u64 front_gidx0;  // gidx of frontier[0]
+  u64* slots;
+  int log2;
+  u64* states_out;  // next level (store + level_base[d+1])
+  u64* parents_out;
+  u64 cap_out;      // room for new states
+  u64* slot_out;    // TLC order: FPSet slot of every new state
+  u64* dkey_slot;   // TLC order: min discovery key per FPSet slot
+  LevelCtr* ctr;
+  u64 rank_tag;     // rank << 56
+  int rank, world;
+  u64 owner_mask;
+  u64* outbox;      // world > 1: [world][outbox_cap] records {state, parent_ref}
+  u64 outbox_cap;
+};
 
 __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
 #pragma unroll

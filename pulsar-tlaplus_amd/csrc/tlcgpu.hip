@@ -13,12 +13,14 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "component.h"
 #include "host_model.h"
+#include "jit.h"
 #include "kernels.h"
 #include "tlcgpu.h"
 
@@ -477,6 +479,11 @@ struct tlcg_ctx {
   unsigned long long* h_comp = nullptr;
   u64* d_ovf[2] = {nullptr, nullptr};
   u64 ovf_cap = 0;
+  // layout-specialized kernels (jit.cpp): 0 untried, 1 built, -1 failed (precompiled ones used)
+  JitKernels jit;
+  int jit_state = 0;
+  bool jit_used = false;
+  std::string jit_error;
   u64 pending = 0;      // states appended to the current level, not yet committed
   // kernel variant (tuning; env TLCG_FAST_ITEMS / TLCG_PROBE / TLCG_GRID)
   int fast_items = 2;   // parents per thread in k_expand_fast (0 = general kernel)
@@ -645,6 +652,7 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
                       : (depth ? c->level_base[(size_t)depth] - c->level_base[(size_t)depth - 1] : 0);
   st->depth = depth;
   st->engine = (uint64_t)c->engine;
+  st->reserved[0] = c->jit_used ? 1 : 0;  // layout-specialized kernels ran
   st->status = c->status;
   st->invariant = -1;
   st->action = -1;
@@ -824,6 +832,16 @@ int run_component(tlcg_ctx* c) {
   c->comp_generated = c->comp_distinct = c->comp_store_used = 0;
   c->pending = 0;
   if (!comp_scratch(c, std::max<u64>(r1 - r0, 1))) return -1;
+  // specialize the kernels for these constants when the run is large enough
+  // to repay a hipRTC compile (env TLCG_JIT=0/1 forces)
+  const char* jv = std::getenv("TLCG_JIT");
+  const bool want_jit = jv ? std::atoi(jv) != 0 : (r1 - r0) >= 65536;
+  if (want_jit && c->jit_state == 0) {
+    std::string e;
+    c->jit_state = jit_build(L, c->opts.device, &c->jit, &e) ? 1 : -1;
+    if (c->jit_state < 0) c->jit_error = e;
+  }
+  c->jit_used = want_jit && c->jit_state == 1;
   static const int kCascade[3] = {64, 128, 255};
   u64 n = r1 - r0;
   int cur = -1;  // overflow list holding this pass's components (-1: range)
@@ -857,7 +875,7 @@ int run_component(tlcg_ctx* c) {
     a.ovf_n = c->d_comp + COMP_MAXLV + 3;
     a.ovf_list = c->d_ovf[out];
     HIPCHK(hipEventRecord(c->e0, c->stream));
-    if (!launch_component(a, K, c->stream)) {
+    if (!(c->jit_used ? jit_launch_component(c->jit, a, K, c->stream) : launch_component(a, K, c->stream))) {
       c->err = "component kernel launch failed";
       return -1;
     }
@@ -1172,6 +1190,7 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_inbox);
   hipFree(c->d_ctr);
   hipFree(c->d_aux);
+  jit_release(&c->jit);
   hipFree(c->d_comp);
   hipFree(c->d_ovf[0]);
   hipFree(c->d_ovf[1]);
@@ -1323,6 +1342,19 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
   }
   if (len) *len = n;
   return 0;
+}
+
+int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t cap) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -1;
+  std::vector<char> code;
+  if (!jit_compile(hm.L, arch ? arch : "gfx950", &code, &e)) {
+    if (err && cap > 0) std::snprintf(err, (size_t)cap, "%s", e.c_str());
+    return -2;
+  }
+  if (err && cap > 0) err[0] = 0;
+  return (int)code.size();
 }
 
 int tlcg_owner(tlcg_ctx* c, uint64_t state) {

@@ -94,6 +94,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_absorb": (C.c_int, [P, U64, S]),
         "tlcg_end_level": (C.c_int, [P, S]),
         "tlcg_stream": (P, [P]),
+        "tlcg_jit_selftest": (C.c_int, [M, C.c_char_p, I32, C.c_char_p, I32][:1] + [C.c_char_p, C.c_char_p, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
