@@ -34,6 +34,8 @@ BYTES_PER_STATE_WORD = 8
 
 
 PMC_PROFILE = "profiles/r01_pmc_k_expand.json"
+PMC_COMPONENT_PROFILE = "profiles/r01_pmc_component.json"
+COMPONENT_BYTES_PER_STATE = 16  # state word + parent entry written to the HBM store
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
 
 
@@ -136,93 +138,117 @@ def main():
 
     cfg = CONFIGS[args.config]
     model = model_for(args.config)
-    per_rank = cfg["distinct"] // world + 1
-    log2 = max(16, (2 * per_rank - 1).bit_length())
-    cap = int(per_rank * 1.08) + 2 * (cfg["distinct"] // 12) // world + (1 << 20)
     import dist as tdist
-    eng = tdist.GpuEngine(model, rank, world, gpu, log2_fpset_slots=log2, state_capacity=cap)
-    assert eng.closed
 
-    def step():
-        return eng.run_closed()
+    def time_engine(engine):
+        """warmup + K timed complete checks with one engine; max over ranks"""
+        per_rank = cfg["distinct"] // world + 1
+        log2 = max(16, (2 * per_rank - 1).bit_length()) if engine == "global" else 0
+        cap = int(per_rank * 1.08) + 2 * (cfg["distinct"] // 12) // world + (1 << 20)
+        eng = tdist.GpuEngine(model, rank, world, gpu, log2_fpset_slots=log2, state_capacity=cap, engine=engine)
+        assert eng.closed
+        for _ in range(args.warmup):
+            eng.run_closed()
+        torch.cuda.synchronize(dev)
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        kms = ems = 0.0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            st = eng.run_closed()
+            ems += st.expand_ms
+            kms += st.kernel_ms
+        torch.cuda.synchronize(dev)
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        counts = [st.generated, st.distinct]
+        used = tlcgpu.ENGINE_NAMES.get(int(st.engine), "?")
+        jit = int(st.reserved[0])
+        launches = len(eng.level_sizes()) if used == "global" else 1
+        if distributed:
+            t = torch.tensor([elapsed, ems, kms], dtype=torch.float64, device=rdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, ems, kms = [float(x) for x in t.tolist()]
+            c = torch.tensor(counts, dtype=torch.int64, device=rdev)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            counts = [int(x) for x in c.tolist()]
+        eng.close()
+        if tuple(counts) != (cfg["generated"], cfg["distinct"]):
+            raise SystemExit(f"count mismatch ({engine}): {counts} want {cfg}")
+        return dict(engine=used, jit=jit, elapsed=elapsed, expand_ms=ems / args.steps, kernel_ms=kms / args.steps,
+                    launches=launches)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    expand_ms = kernel_ms = 0.0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st = step()
-        expand_ms += st.expand_ms
-        kernel_ms += st.kernel_ms
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    levels = eng.level_sizes()
-    launches = len(levels)  # one expand launch per level (the last finds nothing new)
-    local = [st.generated, st.distinct]
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor(local, dtype=torch.int64, device=rdev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        local = [int(x) for x in c.tolist()]
-        e = torch.tensor([expand_ms, kernel_ms], dtype=torch.float64, device=rdev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        expand_ms, kernel_ms = [float(x) for x in e.tolist()]
-    generated, distinct = local
-    if (generated, distinct) != (cfg["generated"], cfg["distinct"]):
-        raise SystemExit(f"count mismatch: {generated} generated, {distinct} distinct, want {cfg}")
+    main_run = time_engine("auto")
+    global_run = time_engine("global")
     if rank != 0:
         if distributed:
             dist.destroy_process_group()
         return
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = distinct * args.steps / elapsed
+    distinct, generated = cfg["distinct"], cfg["generated"]
     n_init = (cfg["keys"] + 1) ** 6
-    # stuttering successors (no FPSet probe): counted on one message sequence,
-    # every sequence has the same compactor graph (SURVEY App.A.1)
     selfloops = n_init * selfloops_per_m(model)
-    bytes_step = algorithmic_bytes(distinct, generated, n_init, selfloops) / world  # per rank
-    expand_ms_step = expand_ms / args.steps
-    achieved = bytes_step / (expand_ms_step * 1e-3) / 1e9
-    avg_launch_s = expand_ms_step / launches * 1e-3
-    roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                    kernel="k_expand", launches_per_step=launches,
-                    avg_launch_ms=round(expand_ms_step / launches, 4),
-                    bytes_per_distinct=round(algorithmic_bytes(distinct, generated, n_init, selfloops) / distinct, 2))
-    pmc = load_profile(PMC_PROFILE)
-    if pmc and args.config == "g9" and world == 1:
-        # HBM bytes booked by FETCH_SIZE + WRITE_SIZE for k_expand (scripts/pmc.sh, calibrated)
-        roofline["traffic"] = round(pmc["hbm_bytes_per_launch"] / avg_launch_s / 1e9, 1)
-        roofline["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_launch"])
-        roofline["traffic_source"] = PMC_PROFILE
-    micro = load_microbench(MICRO_PROFILE)
-    if micro:
-        # the kernel's real ceiling: scattered 8-B FPSet probes and inserts at the
-        # rates measured on a 16 GiB table (pulsar-tlaplus_amd/bin/fpset_microbench)
-        probes = (generated - n_init - selfloops) / world
-        inserts = (distinct - n_init) / world
-        bound_ms = (probes / micro["load_nt"] + inserts / micro["cas_new"]) * 1e3
-        roofline["scattered_access_roofline"] = dict(
-            probes_per_step=int(probes), inserts_per_step=int(inserts),
-            load_per_s=micro["load_nt"], cas_per_s=micro["cas_new"], bound_ms_per_step=round(bound_ms, 2),
-            frac=round(bound_ms / expand_ms_step, 3), source=MICRO_PROFILE)
+
+    def roofline_global(r):
+        bytes_step = algorithmic_bytes(distinct, generated, n_init, selfloops) / world  # per rank
+        achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
+        rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel="k_expand_fast",
+                  launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
+                  bytes_per_distinct=round(algorithmic_bytes(distinct, generated, n_init, selfloops) / distinct, 2))
+        pmc = load_profile(PMC_PROFILE)
+        avg_launch_s = r["expand_ms"] / r["launches"] * 1e-3
+        if pmc and args.config == "g9" and world == 1:
+            rf["traffic"] = round(pmc["hbm_bytes_per_launch"] / avg_launch_s / 1e9, 1)
+            rf["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_launch"])
+            rf["traffic_source"] = PMC_PROFILE
+        micro = load_microbench(MICRO_PROFILE)
+        if micro:
+            probes = (generated - n_init - selfloops) / world
+            inserts = (distinct - n_init) / world
+            bound_ms = (probes / micro["load_nt"] + inserts / micro["cas_new"]) * 1e3
+            rf["scattered_access_roofline"] = dict(
+                probes_per_step=int(probes), inserts_per_step=int(inserts), load_per_s=micro["load_nt"],
+                cas_per_s=micro["cas_new"], bound_ms_per_step=round(bound_ms, 2),
+                frac=round(bound_ms / r["expand_ms"], 3), source=MICRO_PROFILE)
+        return rf
+
+    def roofline_component(r):
+        # the component kernel's only HBM traffic: write each state word and its parent entry
+        bytes_step = COMPONENT_BYTES_PER_STATE * distinct / world
+        achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
+        rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                  kernel="tlcg_component_64 (hipRTC-specialized)" if r["jit"] else "k_component<64>",
+                  launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
+                  bytes_per_distinct=COMPONENT_BYTES_PER_STATE)
+        pmc = load_profile(PMC_COMPONENT_PROFILE)
+        if pmc and args.config == "g9" and world == 1 and r["jit"]:
+            rf["traffic"] = round(pmc["hbm_bytes_per_step"] / (r["expand_ms"] * 1e-3) / 1e9, 1)
+            rf["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_step"])
+            rf["traffic_source"] = PMC_COMPONENT_PROFILE
+            rf["issue"] = dict(valu_insts_per_state=round(pmc["valu_insts_per_state"], 1),
+                               salu_insts_per_state=round(pmc["salu_insts_per_state"], 1),
+                               note="issue/latency-bound on chip (LDS FPSet), not HBM-bound")
+        return rf
+
+    def summary(r):
+        return dict(engine=r["engine"], jit=bool(r["jit"]), value=round(distinct * args.steps / r["elapsed"], 1),
+                    ms_per_step=round(r["elapsed"] * 1e3 / args.steps, 3),
+                    gpu_kernel_ms_per_step=round(r["kernel_ms"], 3),
+                    roofline=roofline_component(r) if r["engine"] == "component" else roofline_global(r))
+
+    main_s, glob_s = summary(main_run), summary(global_run)
     line = {
         "metric": "distinct states/sec, compaction.tla scaled cfg, 1/2/4/8 MI355X vs host TLC",
-        "value": round(value, 1),
+        "value": main_s["value"],
         "unit": "distinct states/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step": main_s["ms_per_step"],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -231,15 +257,15 @@ def main():
         "config": {"workload": f"compaction.tla BFS, {args.config.upper()} cfg: KeySpace = ValueSpace = "
                                f"{{1..{cfg['keys']}}}, MessageSentLimit 3, CompactionTimesLimit 3, MaxCrashTimes 1, "
                                f"RetainNullKey, no producer/consumer",
-                   "distinct": distinct, "generated": generated, "depth": len(levels),
-                   "parallelism": f"fpset-partition{world}", "fpset_slots_log2": log2,
-                   "gpu_kernel_ms_per_step": round(kernel_ms / args.steps, 3)},
-        "roofline": roofline,
+                   "distinct": distinct, "generated": generated, "depth": cfg["depth"],
+                   "parallelism": f"partition{world}", "engine": main_s["engine"],
+                   "gpu_kernel_ms_per_step": main_s["gpu_kernel_ms_per_step"]},
+        "roofline": main_s["roofline"],
+        "engines": {"global_hbm_fpset": glob_s},
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config)
     print(json.dumps(line), flush=True)
-    eng.close()
     if distributed:
         dist.destroy_process_group()
 

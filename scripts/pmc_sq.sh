@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counters of the component kernel on G9 (one group per rocprofv3 pass)
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out/sq
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; export TLCG_JIT=1; mkdir -p gpurun_out/sq
 cat > /tmp/one.py <<'PY'
 import os, sys
 sys.path.insert(0, os.path.join(os.environ["GRAFT_REPO_ROOT"], "pulsar-tlaplus_amd", "python"))
@@ -20,7 +20,7 @@ import csv, glob, collections
 for d in sorted(glob.glob("gpurun_out/sq/p*/run_counter_collection.csv")):
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(d)):
-        if "k_component" in r["Kernel_Name"]:
+        if "component" in r["Kernel_Name"]:
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
     for k, v in agg.items(): print(k, "%.4g" % v)
 PY
