@@ -19,7 +19,8 @@ bool launch_component(const CompArgs& a, int K, hipStream_t stream) {
   if (!a.n_comp) return true;
   const u64 batches = (a.n_comp + 63) / 64;
   const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
-  if (K == 64) k_component<64><<<grid, 64, 0, stream>>>(a);
+  if (K == 32) k_component<32><<<grid, 64, 0, stream>>>(a);
+  else if (K == 64) k_component<64><<<grid, 64, 0, stream>>>(a);
   else if (K == 128) k_component<128><<<grid, 64, 0, stream>>>(a);
   else k_component<255><<<grid, 64, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess;

@@ -9,26 +9,23 @@
 
 namespace tlcg {
 
-__device__ __forceinline__ unsigned slot_of(uint32_t key, int log2t) { return (key * 0x9E3779B1u) >> (32 - log2t); }
+// slot of a local key in a T-slot table (multiply-shift, T need not be a power of 2)
+template <int T>
+__device__ __forceinline__ unsigned slot_of(uint32_t key) {
+  return (unsigned)(((unsigned long long)(key * 0x9E3779B1u) * (unsigned)T) >> 32);
+}
 
+// on-chip FPSet slots per component: 1.5 x the capacity (load <= 2/3)
 template <int K>
-struct CompShape;
-template <>
-struct CompShape<64> { static constexpr int LOG2T = 7; };
-template <>
-struct CompShape<128> { static constexpr int LOG2T = 8; };
-template <>
-struct CompShape<255> { static constexpr int LOG2T = 9; };
+struct CompShape { static constexpr int T = (K * 3 / 2 + 15) / 16 * 16; };
 
 // the BFS of one wave's components; L is the runtime layout (precompiled
 // kernel) or a constexpr one (jit.cpp), in which case every field folds
 template <int K>
 __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& L) {
-  constexpr int LOG2T = CompShape<K>::LOG2T;
-  constexpr int T = 1 << LOG2T;
+  constexpr int T = CompShape<K>::T;
   __shared__ uint32_t q[K][64];                   // FIFO of local keys (word >> msgs_bits)
   __shared__ uint8_t h[T][64];                    // FPSet: 1 + queue position, 0 = empty
-  __shared__ uint8_t bnd[COMP_MAXLV + 1][64];     // queue position where each level starts
   __shared__ unsigned lvl_sh[COMP_MAXLV];
   const int lane = threadIdx.x;
   const int mb = L.msg_sh + L.N * L.mw;  // `messages` occupies the low mb bits
@@ -39,7 +36,10 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
   for (u64 b = blockIdx.x; b * 64 < a.n_comp; b += gridDim.x) {
     const u64 ci = b * 64 + (u64)lane;
     const bool act = ci < a.n_comp;
-    const u64 idx0 = act ? (a.list ? a.list[ci] : a.comp0 + ci) : 0;
+    // cascade entries carry the levels an earlier pass already counted (bits 40..)
+    const u64 entry = act ? (a.list ? a.list[ci] : a.comp0 + ci) : 0;
+    const u64 idx0 = entry & ((1ull << 40) - 1);
+    const int counted = (int)(entry >> 40);
     // clear this wave's FPSet with 16-B stores across the whole [T][64] array
     for (int i = lane; i < T * 64 / 16; i += 64) reinterpret_cast<uint4*>(&h[0][0])[i] = make_uint4(0, 0, 0, 0);
     const u64 s0 = init_state(L, idx0);
@@ -47,13 +47,13 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     u64* st = a.store + b * (u64)K * 64 + (u64)lane;
     u64* par = a.parents + b * (u64)K * 64 + (u64)lane;
     const u64 gbase = a.store_base + b * (u64)K * 64 + (u64)lane;
-    int head = 0, tail = 0, level = 0, lvl_end = 0;
+    int head = 0, tail = 0, level = 0, lvl_end = 0, lvl_start = 0;
     bool alive = act, ovf = false;
     u64 lgen = 0;
     u64 lev = NO_EVENT;
     if (act) {
       const uint32_t k0 = (uint32_t)(s0 >> mb);
-      h[slot_of(k0, LOG2T)][lane] = 1;
+      h[slot_of<T>(k0)][lane] = 1;
       q[0][lane] = k0;
       tail = 1;
       st[0] = s0;
@@ -65,17 +65,16 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
         alive = false;
       }
     }
-    bnd[0][lane] = 0;
     lvl_end = tail;
     // visit one successor: FPSet lookup, insert, invariants (TLC's FPSet.put + check)
     auto visit = [&](u64 t, int action, int pos) {
       const uint32_t key = (uint32_t)(t >> mb);
-      unsigned sl = slot_of(key, LOG2T);
+      unsigned sl = slot_of<T>(key);
       for (int p = 0; p < T; ++p) {
         const unsigned e = h[sl][lane];
         if (e == 0) break;
         if (q[e - 1][lane] == key) return;  // seen
-        sl = (sl + 1) & (T - 1);
+        sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
       }
       if (tail >= K) {  // does not fit on chip: cascade
         ovf = true;
@@ -98,7 +97,14 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       int nsucc = 0;
       u64 t = 0;
       int action = 0;
-      const int r = compactor_step(L, s, &t, &action);  // compaction.tla:221-226
+      // compaction.tla:221-226.  The components of a wave usually sit in the
+      // same compactor phase: dispatch on a wave-uniform phase when they do
+      // (scalar branches), per lane otherwise.
+      const int ph = st_phase(L, s);
+      const int ph0 = __builtin_amdgcn_readfirstlane(ph);
+      int r;
+      if (__all(ph == ph0)) r = compactor_step_ph(L, s, ph0, &t, &action);
+      else r = compactor_step_ph(L, s, ph, &t, &action);
       if (r == 2) {
         lev = min(lev, make_comp_event(level + 1, idx0, head, action, EVK_ACTION_ERROR, action));
         alive = false;
@@ -121,28 +127,33 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       }
       if (!alive) break;
       ++head;
-      if (head == lvl_end) {
+      if (head == lvl_end) {  // level `level` = [lvl_start, lvl_end) is complete
+        if (level >= counted) atomicAdd(&lvl_sh[level], (unsigned)(lvl_end - lvl_start));
         ++level;
         if (level >= COMP_MAXLV) {
           ovf = true;
           break;
         }
-        bnd[level][lane] = (uint8_t)head;  // the new level is [head, tail)
+        lvl_start = head;  // the new level is [head, tail)
         lvl_end = tail;
       }
     }
     if (act && ovf) {
+      // the next pass redoes the component and counts only levels >= `level`
+      // (the complete ones were counted here, at their transitions)
       const unsigned long long k = atomicAdd(a.ovf_n, 1ull);
-      a.ovf_list[k] = idx0;
+      a.ovf_list[k] = idx0 | ((u64)(level > counted ? level : counted) << 40);
     } else if (act) {
       gen += lgen;
       dist += (u64)tail;
       ev = min(ev, (unsigned long long)lev);
-      // levels 0..level-1 are complete; `level` is [bnd[level], lvl_end); a lane
-      // stopped by an error also has level+1 partly discovered: [lvl_end, tail)
-      for (int l = 0; l < level; ++l) atomicAdd(&lvl_sh[l], (unsigned)(bnd[l + 1][lane] - bnd[l][lane]));
-      if (level < COMP_MAXLV && lvl_end > bnd[level][lane]) atomicAdd(&lvl_sh[level], (unsigned)(lvl_end - bnd[level][lane]));
-      if (level + 1 < COMP_MAXLV && tail > lvl_end) atomicAdd(&lvl_sh[level + 1], (unsigned)(tail - lvl_end));
+      // a lane stopped by an error: `level` = [lvl_start, lvl_end) is partly
+      // expanded and level+1 = [lvl_end, tail) partly discovered
+      if (lev != NO_EVENT) {
+        if (level < COMP_MAXLV && level >= counted) atomicAdd(&lvl_sh[level], (unsigned)(lvl_end - lvl_start));
+        if (level + 1 < COMP_MAXLV && level + 1 >= counted && tail > lvl_end)
+          atomicAdd(&lvl_sh[level + 1], (unsigned)(tail - lvl_end));
+      }
     }
   }
   gen = wave_sum_u64(gen);

@@ -39,7 +39,7 @@ std::string program_source(const Layout& L) {
                   "typedef unsigned long uint64_t; typedef long int64_t;\n";
   s += kJitSource;
   s += "\n" + layout_literal(L);
-  for (int K : {64, 128, 255})
+  for (int K : {32, 64, 128, 255})
     s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_component_" + std::to_string(K) +
          "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ">(a, kL); }\n";
   return s;
@@ -131,8 +131,8 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
     *err = "hipModuleLoadData failed for the specialized kernels";
     return false;
   }
-  const char* names[3] = {"tlcg_component_64", "tlcg_component_128", "tlcg_component_255"};
-  for (int i = 0; i < 3; ++i)
+  const char* names[4] = {"tlcg_component_32", "tlcg_component_64", "tlcg_component_128", "tlcg_component_255"};
+  for (int i = 0; i < 4; ++i)
     if (hipModuleGetFunction(&out->component[i], out->module, names[i]) != hipSuccess) {
       *err = std::string("hipModuleGetFunction ") + names[i];
       return false;
@@ -147,7 +147,7 @@ void jit_release(JitKernels* k) {
 
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, hipStream_t stream) {
   if (!a.n_comp) return true;
-  const int i = K == 64 ? 0 : K == 128 ? 1 : 2;
+  const int i = K == 32 ? 0 : K == 64 ? 1 : K == 128 ? 2 : 3;
   const uint64_t batches = (a.n_comp + 63) / 64;
   const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
   CompArgs copy = a;

@@ -13,7 +13,7 @@ namespace tlcg {
 
 struct JitKernels {
   hipModule_t module = nullptr;
-  hipFunction_t component[3] = {nullptr, nullptr, nullptr};  // K = 64, 128, 255
+  hipFunction_t component[4] = {nullptr, nullptr, nullptr, nullptr};  // K = 32, 64, 128, 255
   double compile_s = 0;  // 0 when loaded from the cache
   bool cached = false;
 };

@@ -198,8 +198,7 @@ TLCG_HD u64 producer_succ(const Layout& L, u64 s, int len, int j) {
 // The six compactor disjuncts (compaction.tla:93-165) are mutually exclusive
 // on compactorState, so a state has at most one compactor successor.
 // Returns 0 disabled, 1 enabled (*t, *act set), 2 evaluation error (*act set).
-TLCG_HD int compactor_step(const Layout& L, u64 s, u64* t, int* act) {
-  int ph = st_phase(L, s);
+TLCG_HD int compactor_step_ph(const Layout& L, u64 s, int ph, u64* t, int* act) {
   int p1r = st_p1r(L, s);
   switch (ph) {
     case PH_ONE: {  // CompactorPhaseOne, :93-100
@@ -255,6 +254,10 @@ TLCG_HD int compactor_step(const Layout& L, u64 s, u64* t, int* act) {
     }
   }
   return 0;
+}
+
+TLCG_HD int compactor_step(const Layout& L, u64 s, u64* t, int* act) {
+  return compactor_step_ph(L, s, st_phase(L, s), t, act);
 }
 
 // BrokerCrash, compaction.tla:169-182.  Returns 1 if enabled.

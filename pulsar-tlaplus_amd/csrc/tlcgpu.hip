@@ -760,7 +760,7 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
       if (idx0 >= ps.r0 && idx0 < ps.r0 + ps.n) ci = idx0 - ps.r0;
     } else {
       for (u64 i = 0; i < ps.list.size(); ++i)
-        if (ps.list[i] == idx0) ci = i;
+        if ((ps.list[i] & ((1ull << 40) - 1)) == idx0) ci = i;  // entries carry counted levels above bit 40
     }
     if (ci != NO_PARENT) gidx = ps.store_base + (ci / 64) * (u64)ps.K * 64 + (u64)pos * 64 + (ci % 64);
   }
@@ -842,11 +842,16 @@ int run_component(tlcg_ctx* c) {
     if (c->jit_state < 0) c->jit_error = e;
   }
   c->jit_used = want_jit && c->jit_state == 1;
-  static const int kCascade[3] = {64, 128, 255};
+  // on-chip capacity cascade; the first step is tunable (TLCG_COMP_K0 = 32 / 64)
+  int kCascade[4] = {64, 128, 255, 0};
+  if (const char* k0 = std::getenv("TLCG_COMP_K0"))
+    if (std::atoi(k0) == 32) {
+      kCascade[0] = 32; kCascade[1] = 64; kCascade[2] = 128; kCascade[3] = 255;
+    }
   u64 n = r1 - r0;
   int cur = -1;  // overflow list holding this pass's components (-1: range)
   u64 best_ev = NO_EVENT;
-  for (int p = 0; p < 3 && n; ++p) {
+  for (int p = 0; p < 4 && kCascade[p] && n; ++p) {
     const int K = kCascade[p];
     const u64 base = c->comp_store_used;
     const u64 slots = component_store_slots(n, K);

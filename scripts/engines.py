@@ -3,7 +3,9 @@ import os, sys, time, json
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'pulsar-tlaplus_amd', 'python'))
 import tlcgpu as T
 m = T.Model(key_space=range(1, 16), value_space=range(1, 16))
-for eng, jit in (("component", "1"), ("component", "0"), ("global", "0")):
+which = sys.argv[1] if len(sys.argv) > 1 else "all"
+runs = (("component", "1"), ("component", "0"), ("global", "0")) if which == "all" else (("component", "1"),)
+for eng, jit in runs:
     os.environ["TLCG_JIT"] = jit
     t0 = time.perf_counter()
     ck = T.Checker(m, engine=eng, state_capacity=1_200_000_000, log2_fpset_slots=31 if eng == "global" else 0)

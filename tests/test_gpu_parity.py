@@ -188,3 +188,15 @@ def test_component_engine_multi_rank_ranges():
         finally:
             ck.close()
     assert (tot_g, tot_d) == (want["generated"], want["distinct"])
+
+
+@pytest.mark.parametrize("case", ["S", "R_C4_K1", "R_C5_K1", "R_C4_K3", "V_leak", "V_dup", "X_keys3_vals57",
+                                  "D_N0_K1", "S_consumer"])
+def test_component_cascade(case, monkeypatch):
+    # start the on-chip cascade at 32 states per component: components of
+    # 33..255 states overflow and are redone at 64/128/255; levels counted before
+    # the overflow are not counted twice
+    monkeypatch.setenv("TLCG_COMP_K0", "32")
+    m = model_of(GOLDEN[case]["constants"])
+    r = tlcgpu.run(m)
+    check_against_golden(case, r, False)
