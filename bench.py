@@ -181,8 +181,47 @@ def main():
         return dict(engine=used, jit=jit, elapsed=elapsed, expand_ms=ems / args.steps, kernel_ms=kms / args.steps,
                     launches=launches)
 
+    def time_exchange():
+        """BASELINE config 4: the global engine with the FPSet hash-partitioned on
+        the whole state (partition 2), so successors cross ranks and every BFS
+        level runs expand -> all-to-all of {state, parent} records (RCCL over
+        xGMI) -> absorb -> all-reduce (dist.run)."""
+        per_rank = cfg["distinct"] // world + 1
+        log2 = max(16, (2 * per_rank - 1).bit_length())
+        cap = int(per_rank * 1.1) + (1 << 20)
+        eng = tdist.GpuEngine(model, rank, world, gpu, log2_fpset_slots=log2, state_capacity=cap, engine="global",
+                              partition=2)
+        assert not eng.closed
+        for _ in range(args.warmup):
+            tdist.run(eng, dev=rdev)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        timing = {}
+        k0 = eng.stats.kernel_ms
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            r = tdist.run(eng, dev=rdev, timing=timing)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        t = torch.tensor([elapsed, timing.get("exchange_s", 0.0)], dtype=torch.float64, device=rdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        eng.close()
+        if (r.generated, r.distinct, r.depth) != (cfg["generated"], cfg["distinct"], cfg["depth"]):
+            raise SystemExit(f"count mismatch (exchange): {(r.generated, r.distinct, r.depth)} want {cfg}")
+        return dict(engine="global", partition="whole state (owner = mix64(state))",
+                    exchange="all_to_all_single per level, " + dist.get_backend(),
+                    value=round(cfg["distinct"] * args.steps / float(t[0]), 1),
+                    ms_per_step=round(float(t[0]) * 1e3 / args.steps, 3),
+                    exchange_ms_per_step=round(float(t[1]) * 1e3 / args.steps, 3))
+
     main_run = time_engine("auto")
     global_run = time_engine("global")
+    exchange_run = None
+    if distributed and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
+        exchange_run = time_exchange()
     if rank != 0:
         if distributed:
             dist.destroy_process_group()
@@ -263,6 +302,8 @@ def main():
         "roofline": main_s["roofline"],
         "engines": {"global_hbm_fpset": glob_s},
     }
+    if exchange_run:
+        line["engines"]["global_open_partition_alltoall"] = exchange_run
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config)
     print(json.dumps(line), flush=True)

@@ -185,6 +185,12 @@ int tlcg_outbox(tlcg_ctx* c, int32_t dst, void** dev_records, uint64_t* n_record
 int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records);
 int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st);
 int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st);
+/* Stream-ordered forms of the exchange copies: the first n records for dst
+ * copied to caller memory (host or device), and the caller's n records (host
+ * or device) copied in and absorbed.  The raw tlcg_outbox/tlcg_inbox pointers
+ * need the caller to order its own copies against the context's stream. */
+int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n);
+int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats* st);
 
 /* Diagnostic: compile the kernels specialized for these constants (hipRTC)
  * for `arch` without a device; returns the code-object size or <0 (err). */

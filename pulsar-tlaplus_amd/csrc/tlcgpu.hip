@@ -522,6 +522,15 @@ namespace {
       return false;                                                               \
     }                                                                             \
   } while (0)
+// the same for the int-returning entry points (< 0 = error)
+#define HIPCHK_I(expr)                                                            \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      c->err = std::string(#expr) + ": " + hipGetErrorString(_e);                 \
+      return -10;                                                                 \
+    }                                                                             \
+  } while (0)
 
 u64 distinct_of(const tlcg_ctx* c) { return c->level_base.empty() ? 0 : c->level_base.back(); }
 // first unused slot of the state store
@@ -859,11 +868,11 @@ int run_component(tlcg_ctx* c) {
     tlcg_ctx::CompPass pass{K, base, r0, n, {}};
     if (cur >= 0) {
       pass.list.resize(n);
-      HIPCHK(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
+      HIPCHK_I(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
     }
     const int out = cur == 0 ? 1 : 0;
-    HIPCHK(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * (COMP_MAXLV + 4), c->stream));
-    HIPCHK(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
+    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * (COMP_MAXLV + 4), c->stream));
+    HIPCHK_I(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
     CompArgs a;
     a.L = L;
     a.comp0 = r0;
@@ -879,15 +888,15 @@ int run_component(tlcg_ctx* c) {
     a.event = c->d_comp + COMP_MAXLV + 2;
     a.ovf_n = c->d_comp + COMP_MAXLV + 3;
     a.ovf_list = c->d_ovf[out];
-    HIPCHK(hipEventRecord(c->e0, c->stream));
+    HIPCHK_I(hipEventRecord(c->e0, c->stream));
     if (!(c->jit_used ? jit_launch_component(c->jit, a, K, c->stream) : launch_component(a, K, c->stream))) {
       c->err = "component kernel launch failed";
       return -1;
     }
-    HIPCHK(hipEventRecord(c->e1, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * (COMP_MAXLV + 4),
+    HIPCHK_I(hipEventRecord(c->e1, c->stream));
+    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * (COMP_MAXLV + 4),
                           hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK_I(hipStreamSynchronize(c->stream));
     float ms = 0;
     hipEventElapsedTime(&ms, c->e0, c->e1);
     c->kernel_ms += ms;
@@ -936,7 +945,7 @@ bool run_init(tlcg_ctx* c) {
   }
   for (;;) {
     if (!reset_ctr(c)) return false;
-    HIPCHK(hipEventRecord(c->e0, c->stream));
+    HIPCHK_I(hipEventRecord(c->e0, c->stream));
     if (world == 1) {
       k_init_direct<<<grid_for(hm.n_init, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
           L, hm.n_init, c->d_slots, c->log2, c->d_states, c->d_parents, c->d_ctr);
@@ -945,8 +954,8 @@ bool run_init(tlcg_ctx* c) {
           L, hm.n_init, c->opts.rank, world, c->owner_mask, c->d_slots, c->log2, c->d_states, c->d_parents,
           c->cap, c->d_ctr);
     }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->e1, c->stream));
+    HIPCHK_I(hipGetLastError());
+    HIPCHK_I(hipEventRecord(c->e1, c->stream));
     if (!read_ctr(c)) return false;
     float ms = 0;
     hipEventElapsedTime(&ms, c->e0, c->e1);
@@ -1013,7 +1022,7 @@ bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
       else if (it == 2) k_expand_fast<2, 1><<<g, BLOCK, 0, c->stream>>>(a);
       else k_expand_fast<4, 1><<<g, BLOCK, 0, c->stream>>>(a);
     }
-    HIPCHK(hipGetLastError());
+    HIPCHK_I(hipGetLastError());
     return true;
   }
   const u64 per_block = (u64)BLOCK * (prod ? 1 : ITEMS);
@@ -1027,7 +1036,7 @@ bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
     else if (part) launch_expand_t<false, false, true>(a, grid, c->stream);
     else launch_expand_t<false, false, false>(a, grid, c->stream);
   }
-  HIPCHK(hipGetLastError());
+  HIPCHK_I(hipGetLastError());
   return true;
 }
 
@@ -1039,14 +1048,14 @@ bool tlc_order_level(tlcg_ctx* c, u64 n_new) {
   const u64 d = distinct_of(c);
   k_gather_dkey<<<grid_for(n_new, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(n_new, c->d_slot_new,
                                                                               c->d_dkey_slot, c->d_dk);
-  HIPCHK(hipGetLastError());
+  HIPCHK_I(hipGetLastError());
   const int end_bit = std::min(64, bits_for(((d + n_new) << L.ord_bits) | ((1ull << L.ord_bits) - 1)));
   size_t tmp = c->sort_tmp_bytes;
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, c->d_states + d, c->d_st2,
+  HIPCHK_I(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, c->d_states + d, c->d_st2,
                                             (int)n_new, 0, end_bit, c->stream));
   k_tlc_finish<<<grid_for(n_new, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
       L, n_new, c->d_st2, c->d_dk2, c->d_states + d, c->d_parents + d, (u64)c->opts.rank << 56, c->d_ctr);
-  HIPCHK(hipGetLastError());
+  HIPCHK_I(hipGetLastError());
   return true;
 }
 
@@ -1082,15 +1091,15 @@ bool step_level(tlcg_ctx* c) {
   if (!ensure_scratch(c, std::min(worst, c->cap - d))) return false;
   for (;;) {
     if (!reset_ctr(c)) return false;
-    HIPCHK(hipEventRecord(c->e0, c->stream));
+    HIPCHK_I(hipEventRecord(c->e0, c->stream));
     if (!launch_expand(c, f0, F, false)) return false;
-    HIPCHK(hipEventRecord(c->e1, c->stream));
+    HIPCHK_I(hipEventRecord(c->e1, c->stream));
     if (c->opts.tlc_order) {
       // n_new is needed on the host to size the sort
       if (!read_ctr(c)) return false;
       if (!c->h_ctr->overflow && !tlc_order_level(c, c->h_ctr->n_new)) return false;
     }
-    HIPCHK(hipEventRecord(c->e2, c->stream));
+    HIPCHK_I(hipEventRecord(c->e2, c->stream));
     if (!read_ctr(c)) return false;
     float ms_exp = 0, ms_all = 0;
     hipEventElapsedTime(&ms_exp, c->e0, c->e1);
@@ -1483,6 +1492,29 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
   c->pending = c->h_ctr->n_new;
   fill_stats(c, st);
   return 0;
+}
+
+// Copy the first n records for `dst` to caller memory (host or device; the
+// runtime infers which), ordered after the expand on the context's stream.
+int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n) {
+  if (!c || dst < 0 || dst >= c->opts.world || dst == c->opts.rank) return -1;
+  if (!n) return 0;
+  if (!c->d_outbox || n > c->h_ctr->n_out[dst] || n > c->outbox_cap) return -1;
+  HIPCHK_I(hipMemcpyAsync(out, c->d_outbox + 2 * (u64)dst * c->outbox_cap, n * 16, hipMemcpyDefault, c->stream));
+  HIPCHK_I(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// tlcg_inbox + copy + tlcg_absorb in one call: the copy of the caller's
+// records (host or device) and the insert run in order on the context's stream.
+int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats* st) {
+  if (!c) return -1;
+  if (n) {
+    const int r = tlcg_inbox(c, n, nullptr);
+    if (r) return r;
+    HIPCHK_I(hipMemcpyAsync(c->d_inbox, records, n * 16, hipMemcpyDefault, c->stream));
+  }
+  return tlcg_absorb(c, n, st);
 }
 
 int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st) {

@@ -45,19 +45,6 @@ class DistResult:
     closed: bool
 
 
-_hip = None
-
-
-def _hip_memcpy(dst: int, src: int, nbytes: int):
-    global _hip
-    if _hip is None:
-        _hip = C.CDLL("libamdhip64.so")
-        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-        _hip.hipMemcpy.restype = C.c_int
-    if nbytes and _hip.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, 3) != 0:  # DeviceToDevice
-        raise RuntimeError("hipMemcpy failed")
-
-
 class GpuEngine:
     """One rank's libtlcgpu context (the partitioned C-ABI)."""
 
@@ -83,20 +70,23 @@ class GpuEngine:
         return counts
 
     def outbox(self, dst: int) -> torch.Tensor:
+        """This rank's records for `dst`, copied (in stream order) to a new tensor."""
         p, n = C.c_void_p(), C.c_uint64()
         self.lib.tlcg_outbox(self.ctx, dst, C.byref(p), C.byref(n))
         t = torch.empty((n.value, 2), dtype=torch.int64, device=f"cuda:{self.device}")
         torch.cuda.synchronize(self.device)
-        _hip_memcpy(t.data_ptr(), p.value or 0, n.value * 16)
+        if n.value:
+            self.ck._chk(self.lib.tlcg_outbox_read(self.ctx, dst, C.c_void_p(t.data_ptr()), n.value),
+                         "tlcg_outbox_read")
         return t
 
     def absorb(self, recs: torch.Tensor):
-        n = recs.shape[0]
-        p = C.c_void_p()
-        self.ck._chk(self.lib.tlcg_inbox(self.ctx, n, C.byref(p)), "tlcg_inbox")
-        torch.cuda.synchronize(self.device)
-        _hip_memcpy(p.value, recs.data_ptr(), n * 16)
-        self.ck._chk(self.lib.tlcg_absorb(self.ctx, n, C.byref(self.stats)), "tlcg_absorb")
+        """Insert records from other ranks (device or host tensor, [n, 2] int64)."""
+        recs = recs.contiguous()
+        if recs.device.type == "cuda":
+            torch.cuda.synchronize(self.device)  # torch's producer of `recs` is done
+        self.ck._chk(self.lib.tlcg_absorb_records(self.ctx, C.c_void_p(recs.data_ptr()), recs.shape[0],
+                                                  C.byref(self.stats)), "tlcg_absorb_records")
 
     def end_level(self):
         self.ck._chk(self.lib.tlcg_end_level(self.ctx, C.byref(self.stats)), "tlcg_end_level")
@@ -137,30 +127,50 @@ def _reduce_result(engine, stats, group, dev: torch.device) -> DistResult:
                       expand_ms=stats.expand_ms, closed=engine.closed)
 
 
-def run(engine, group=None, dev: Optional[torch.device] = None) -> DistResult:
-    """Model-check with every rank of `group` (engine = this rank's share)."""
+def _transport_device(group, dev: torch.device) -> torch.device:
+    """Where exchanged records live: on the GPU for RCCL (nccl backend, xGMI),
+    in host memory for gloo (rehearsals of the same level loop)."""
+    return dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+def run(engine, group=None, dev: Optional[torch.device] = None, timing: Optional[dict] = None) -> DistResult:
+    """Model-check with every rank of `group` (engine = this rank's share).
+
+    `timing`, when given, accumulates the seconds spent in the exchange
+    (outbox gather, the two all-to-alls, inbox copy) under "exchange_s"."""
+    import time
     dev = dev or torch.device("cpu")
     world = dist.get_world_size(group)
     if engine.closed:
         stats = engine.run_closed()
         return _reduce_result(engine, stats, group, dev)
+    xdev = _transport_device(group, dev)
     stats = engine.init()
     me = dist.get_rank(group)
     lv0 = engine.level_sizes()
     flags = torch.tensor([lv0[-1] if lv0 else 0, 1 if stats.status >= 2 else 0], dtype=torch.int64, device=dev)
     dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
+    xs = 0.0
     while not flags[1].item() and flags[0].item():
         counts = engine.expand()
-        # all-to-all: counts, then the records (16 bytes each)
-        send_counts = torch.tensor(counts, dtype=torch.int64, device=dev)
-        recv_counts = torch.empty(world, dtype=torch.int64, device=dev)
+        t0 = time.perf_counter()
+        # all-to-all: counts, then the records (16 bytes each), destination-major
+        send_counts = torch.tensor(counts, dtype=torch.int64, device=xdev)
+        send_counts[me] = 0
+        recv_counts = torch.empty(world, dtype=torch.int64, device=xdev)
         dist.all_to_all_single(recv_counts, send_counts, group=group)
         rc = [int(x) for x in recv_counts.tolist()]
-        sends = [engine.outbox(d) if d != me else engine.new_tensor((0, 2), torch.int64) for d in range(world)]
-        send = torch.cat(sends, 0) if sends else engine.new_tensor((0, 2), torch.int64)
-        recv = engine.new_tensor((sum(rc), 2), torch.int64)
-        sc = [s.shape[0] for s in sends]
+        sc = [int(x) for x in send_counts.tolist()]
+        sends = [engine.outbox(d) if sc[d] else None for d in range(world)]
+        send = torch.empty((sum(sc), 2), dtype=torch.int64, device=xdev)
+        off = 0
+        for d in range(world):
+            if sends[d] is not None:
+                send[off:off + sc[d]].copy_(sends[d])
+                off += sc[d]
+        recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=xdev)
         dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc, group=group)
+        xs += time.perf_counter() - t0
         if recv.shape[0]:
             engine.absorb(recv)
         stats = engine.end_level()
@@ -168,4 +178,6 @@ def run(engine, group=None, dev: Optional[torch.device] = None) -> DistResult:
         lv = engine.level_sizes()
         flags = torch.tensor([lv[-1] if lv else 0, 1 if stats.status >= 2 else 0], dtype=torch.int64, device=dev)
         dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
+    if timing is not None:
+        timing["exchange_s"] = timing.get("exchange_s", 0.0) + xs
     return _reduce_result(engine, stats, group, dev)

@@ -94,6 +94,8 @@ def load_library(path: str = LIB_PATH):
         "tlcg_inbox": (C.c_int, [P, U64, C.POINTER(P)]),
         "tlcg_absorb": (C.c_int, [P, U64, S]),
         "tlcg_end_level": (C.c_int, [P, S]),
+        "tlcg_outbox_read": (C.c_int, [P, I32, P, U64]),
+        "tlcg_absorb_records": (C.c_int, [P, P, U64, S]),
         "tlcg_stream": (P, [P]),
         "tlcg_jit_selftest": (C.c_int, [M, C.c_char_p, I32, C.c_char_p, I32][:1] + [C.c_char_p, C.c_char_p, I32]),
     }
