@@ -173,6 +173,11 @@ uint64_t tlcg_host_init_state(const tlcg_model* m, uint64_t idx);
 int tlcg_host_successors(const tlcg_model* m, uint64_t state, uint64_t* out, int32_t* actions, int32_t cap);
 /* First failing invariant of a state: -1 all hold, else (index << 1) | is_error. */
 int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state);
+/* Self-check of the component engine's specialized evaluators against the
+ * generic ones on the components of initial states [first, first + n), host
+ * only.  Returns the states compared (0: the component engine does not take
+ * this model), or < 0 on a disagreement. */
+int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint64_t n);
 /* Owner rank of a state under the context's partition. */
 int tlcg_owner(tlcg_ctx* c, uint64_t state);
 

@@ -4,6 +4,7 @@
 #pragma once
 #if !defined(__HIPCC_RTC__)
 #include "component.h"
+#include "component_model.h"
 #include "kernels.h"
 #endif
 
@@ -16,8 +17,12 @@ __device__ __forceinline__ unsigned slot_of(uint32_t key) {
 }
 
 // on-chip FPSet slots per component: 1.5 x the capacity (load <= 2/3)
+#ifndef TLCG_FPSET_NUM  // on-chip FPSet slots = K * NUM / DEN (tuning hook, jit.cpp)
+#define TLCG_FPSET_NUM 3
+#define TLCG_FPSET_DEN 2
+#endif
 template <int K>
-struct CompShape { static constexpr int T = (K * 3 / 2 + 15) / 16 * 16; };
+struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN + 15) / 16 * 16; };
 
 // the BFS of one wave's components; L is the runtime layout (precompiled
 // kernel) or a constexpr one (jit.cpp), in which case every field folds
@@ -44,6 +49,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     for (int i = lane; i < T * 64 / 16; i += 64) reinterpret_cast<uint4*>(&h[0][0])[i] = make_uint4(0, 0, 0, 0);
     const u64 s0 = init_state(L, idx0);
     const u64 msgs = s0 & L.msgs_mask;
+    const CompMsgs cmsg = comp_msgs_init(L, s0);  // everything that reads only `messages`
     u64* st = a.store + b * (u64)K * 64 + (u64)lane;
     u64* par = a.parents + b * (u64)K * 64 + (u64)lane;
     const u64 gbase = a.store_base + b * (u64)K * 64 + (u64)lane;
@@ -59,7 +65,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       st[0] = s0;
       par[0] = NO_PARENT;
       lgen = 1;
-      const int c = check_invariants(L, s0);
+      const int c = check_invariants_k(L, cmsg, k0);
       if (c >= 0) {  // an initial state violates: level field 0 sorts before every expansion
         lev = make_comp_event(0, idx0, 0, 0, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1);
         alive = false;
@@ -67,8 +73,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     }
     lvl_end = tail;
     // visit one successor: FPSet lookup, insert, invariants (TLC's FPSet.put + check)
-    auto visit = [&](u64 t, int action, int pos) {
-      const uint32_t key = (uint32_t)(t >> mb);
+    auto visit = [&](lkey key, int action, int pos) {
       unsigned sl = slot_of<T>(key);
       for (int p = 0; p < T; ++p) {
         const unsigned e = h[sl][lane];
@@ -83,28 +88,35 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       }
       h[sl][lane] = (uint8_t)(tail + 1);
       q[tail][lane] = key;
-      st[(u64)tail * 64] = t;
+#ifndef TLCG_NO_STORE  // (experiment only: measures what the HBM store costs)
+      st[(u64)tail * 64] = msgs | ((u64)key << mb);
       par[(u64)tail * 64] = a.rank_tag | ((gbase + (u64)pos * 64) << L.ord_bits) | (u64)ordinal_of(L, action, 0);
+#endif
       ++tail;
-      const int c = check_invariants(L, t);
+      const int c = check_invariants_k(L, cmsg, key);
       if (c >= 0) {
         lev = min(lev, make_comp_event(level + 1, idx0, pos, action, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
         alive = false;
       }
     };
     while (alive && head < tail) {
-      const u64 s = msgs | ((u64)q[head][lane] << mb);
+      const lkey s = q[head][lane];
       int nsucc = 0;
-      u64 t = 0;
+      lkey t = 0;
       int action = 0;
-      // compaction.tla:221-226.  The components of a wave usually sit in the
-      // same compactor phase: dispatch on a wave-uniform phase when they do
-      // (scalar branches), per lane otherwise.
-      const int ph = st_phase(L, s);
+      // compaction.tla:221-226, on the lane's local key.  Per-lane dispatch on
+      // compactorState; TLCG_UNIFORM_PHASE (tuning hook) takes a scalar
+      // branch when the wave agrees (measured no faster).
+      const int ph = k_phase(L, s);
       const int ph0 = __builtin_amdgcn_readfirstlane(ph);
       int r;
-      if (__all(ph == ph0)) r = compactor_step_ph(L, s, ph0, &t, &action);
-      else r = compactor_step_ph(L, s, ph, &t, &action);
+#ifdef TLCG_UNIFORM_PHASE
+      if (__all(ph == ph0)) r = compactor_step_k(L, cmsg, msgs, s, ph0, &t, &action);
+      else r = compactor_step_k(L, cmsg, msgs, s, ph, &t, &action);
+#else
+      r = compactor_step_k(L, cmsg, msgs, s, ph, &t, &action);
+      (void)ph0;
+#endif
       if (r == 2) {
         lev = min(lev, make_comp_event(level + 1, idx0, head, action, EVK_ACTION_ERROR, action));
         alive = false;
@@ -114,12 +126,12 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
         ++nsucc;
         visit(t, action, head);
       }
-      u64 t2 = 0;
-      if (alive && crash_step(L, s, &t2)) {  // BrokerCrash, compaction.tla:227
+      lkey t2 = 0;
+      if (alive && crash_step_k(L, s, &t2)) {  // BrokerCrash, compaction.tla:227
         ++nsucc;
         visit(t2, ACT_CRASH, head);
       }
-      nsucc += selfloop_count(L, s);  // Consumer / Terminating stutters
+      nsucc += selfloop_count_k(L, cmsg, s);  // Consumer / Terminating stutters
       lgen += (u64)nsucc;
       if (alive && nsucc == 0 && L.check_deadlock) {
         lev = min(lev, make_comp_event(level + 1, idx0, head, 15, EVK_DEADLOCK, 0));

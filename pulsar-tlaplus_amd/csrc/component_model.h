@@ -1,0 +1,255 @@
+// pulsar-tlaplus_amd/csrc/component_model.h -- the spec's per-state
+// functions specialized to one component (component.h), on 32-bit local keys.
+//
+// Inside a component `messages` is a constant (no enabled action writes it,
+// compaction.tla:87,100,132,139,145,151,165,182,186,214).  Two consequences:
+//
+// 1. A state is its *local key*: the packed word above the `messages` bits
+//    (model.h layout: ledgers, phaseOneResult, cursor, phase, horizon,
+//    context, crash), k = word >> led_sh.  The component engine admits a
+//    model only when that fits 32 bits, so every transition and invariant
+//    below runs on 32-bit integers.
+// 2. Every sub-expression that reads only `messages` is evaluated once per
+//    component (comp_msgs_init) instead of once per state:
+//      - Len(messages)                               (:57);
+//      - CompactMessages(messages, r) for r = 1..N   (:107-119);
+//      - the messages conjunct of TypeSafe           (:238);
+//      - for CompactionHorizonCorrectness (:259-274), per position i, which
+//        ledger positions witness it: key(p) = key(i) /\ p >= i (an entry's
+//        id is its position), or p = i for a retained null key;
+//      - the null-key positions DuplicateNullKeyMessage (:280-294) reads.
+//
+// The results are exactly model.h's on the word msgs | k << led_sh (same
+// successor, same three-valued invariant outcome in cfg order):
+// tlcg_host_component_selfcheck compares the two on whole components.
+#pragma once
+#if !defined(__HIPCC_RTC__)
+#include "model.h"
+#endif
+
+namespace tlcg {
+
+typedef uint32_t lkey;  // local key
+
+struct CompMsgs {
+  u64 cm;             // CompactMessages for r = 1..N: N bits at (r - 1) * N
+  u64 need;           // horizon witnesses of position i = 1..N: N bits at (i - 1) * N
+  uint32_t skip;      // positions whose messagesBeforeHorizon entry is Nil (null key, not retained)
+  uint32_t null_pos;  // positions 1..Len holding NullKey
+  int len;            // Len(messages)
+  int msgs_ok;        // TypeSafe's messages conjunct (and Len(messages) <= N)
+};
+
+TLCG_HD u64 nmask(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
+TLCG_HD uint32_t lmask(int w) { return w >= 32 ? ~0u : ((1u << w) - 1); }
+
+TLCG_HD CompMsgs comp_msgs_init(const Layout& L, u64 s) {
+  CompMsgs c;
+  c.len = st_len(L, s);
+  c.cm = c.need = 0;
+  c.skip = c.null_pos = 0;
+  c.msgs_ok = c.len <= L.N;
+  // positions 1..N on the raw bits, exactly as model.h reads them
+  for (int i = 1; i <= L.N; ++i) {
+    const int k = st_key(L, s, i);
+    if (i <= c.len && (k >= L.nk || st_val(L, s, i) >= L.nv)) c.msgs_ok = 0;
+    c.cm |= compact_mask(L, s, i) << ((i - 1) * L.N);
+    if (k == 0) {
+      if (i <= c.len) c.null_pos |= 1u << (i - 1);
+      if (L.retain) c.need |= (1ull << (i - 1)) << ((i - 1) * L.N);
+      else c.skip |= 1u << (i - 1);
+    } else {
+      u64 w = 0;
+      for (int p = i; p <= L.N; ++p)
+        if (st_key(L, s, p) == k) w |= 1ull << (p - 1);
+      c.need |= w << ((i - 1) * L.N);
+    }
+  }
+  return c;
+}
+
+// ---- fields of a local key (model.h accessors shifted down by led_sh) ----
+TLCG_HD lkey lget(const Layout& L, lkey k, int sh, int w) { return w ? (k >> (sh - L.led_sh)) & lmask(w) : 0; }
+TLCG_HD lkey lset(const Layout& L, lkey k, int sh, int w, lkey v) {
+  if (!w) return k;
+  const lkey m = lmask(w) << (sh - L.led_sh);
+  return (k & ~m) | ((v << (sh - L.led_sh)) & m);
+}
+TLCG_HD int k_phase(const Layout& L, lkey k) { return (int)lget(L, k, L.ph_sh, 3); }
+TLCG_HD int k_p1r(const Layout& L, lkey k) { return (int)lget(L, k, L.p1r_sh, L.p1r_w); }
+TLCG_HD int k_hz(const Layout& L, lkey k) { return (int)lget(L, k, L.hz_sh, L.hz_w); }
+TLCG_HD int k_ctx(const Layout& L, lkey k) { return (int)lget(L, k, L.ctx_sh, L.ctx_w); }
+TLCG_HD int k_crash(const Layout& L, lkey k) { return (int)lget(L, k, L.cr_sh, L.cr_w); }
+TLCG_HD int k_led_off(const Layout& L, int j1) { return (j1 - 1) * L.led_w; }  // ledger j1, local bit offset
+TLCG_HD int k_led_present(const Layout& L, lkey k, int j1) { return (int)((k >> k_led_off(L, j1)) & 1); }
+TLCG_HD lkey k_led_mask(const Layout& L, lkey k, int j1) { return (k >> (k_led_off(L, j1) + 1)) & lmask(L.N); }
+TLCG_HD lkey k_present_mask(const Layout& L) { return (lkey)(L.led_present_mask >> L.led_sh); }
+TLCG_HD int k_cur_present(const Layout& L, lkey k) { return (int)((k >> (L.cur_sh - L.led_sh)) & 1); }
+TLCG_HD int k_cur_h(const Layout& L, lkey k) { return (int)lget(L, k, L.cur_sh + 1, L.curh_w); }
+TLCG_HD int k_cur_c(const Layout& L, lkey k) { return (int)lget(L, k, L.cur_sh + 1 + L.curh_w, L.curc_w); }
+TLCG_HD int highbit32(uint32_t x) {  // x != 0
+#if defined(__HIP_DEVICE_COMPILE__)
+  return 31 - __clz((int)x);
+#else
+  return 31 - __builtin_clz(x);
+#endif
+}
+TLCG_HD int popcount32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popc(x);
+#else
+  return __builtin_popcount(x);
+#endif
+}
+// MaxCompactedLedgerId, compaction.tla:103-106
+TLCG_HD int k_max_ledger(const Layout& L, lkey k) {
+  const lkey p = k & k_present_mask(L);
+  return p ? highbit32(p) / L.led_w + 1 : 0;
+}
+
+// ---- Next disjuncts on local keys (model.h compactor_step_ph / crash_step) ----
+
+// The compactor disjunct, compaction.tla:93-165.  `full` rebuilds the whole
+// word for the one case that needs more than the precomputed facts.
+// Returns 0 disabled, 1 enabled (*t, *act set), 2 evaluation error (*act set).
+TLCG_HD int compactor_step_k(const Layout& L, const CompMsgs& c, u64 msgs, lkey k, int ph, lkey* t, int* act) {
+  const int p1r = k_p1r(L, k);
+  switch (ph) {
+    case PH_ONE: {  // CompactorPhaseOne, :93-100
+      if (p1r != 0 || c.len <= 0) return 0;
+      *t = lset(L, lset(L, k, L.p1r_sh, L.p1r_w, (lkey)c.len), L.ph_sh, 3, PH_WRITE);
+      *act = ACT_PHASEONE;
+      return 1;
+    }
+    case PH_WRITE: {  // CompactorPhaseTwoWrite, :121-132
+      if (p1r == 0) return 0;
+      const int nid = k_max_ledger(L, k) + 1;
+      if (nid > L.C) return 0;
+      const u64 mask = p1r <= L.N ? (c.cm >> ((p1r - 1) * L.N)) & nmask(L.N)
+                                  : compact_mask(L, msgs | ((u64)k << L.led_sh), p1r);
+      const lkey u = lset(L, k, led_base(L, nid), L.led_w, (lkey)(1ull | (mask << 1)));
+      *t = lset(L, u, L.ph_sh, 3, PH_UCTX);
+      *act = ACT_WRITE;
+      return 1;
+    }
+    case PH_UCTX: {  // CompactorPhaseTwoUpdateContext, :135-139
+      *t = lset(L, lset(L, k, L.ctx_sh, L.ctx_w, (lkey)k_max_ledger(L, k)), L.ph_sh, 3, PH_UHOR);
+      *act = ACT_UCTX;
+      return 1;
+    }
+    case PH_UHOR: {  // CompactorPhaseTwoUpdateHorizon, :141-145
+      *act = ACT_UHOR;
+      if (p1r == 0) return 2;  // phaseOneResult.readPosition of Nil
+      *t = lset(L, lset(L, k, L.hz_sh, L.hz_w, (lkey)p1r), L.ph_sh, 3, PH_PERSIST);
+      return 1;
+    }
+    case PH_PERSIST: {  // CompactorPhaseTwoPersistCusror, :147-151
+      const lkey cur = 1u | ((lkey)k_hz(L, k) << 1) | ((lkey)k_ctx(L, k) << (1 + L.curh_w));
+      *t = lset(L, lset(L, k, L.cur_sh, 1 + L.curh_w + L.curc_w, cur), L.ph_sh, 3, PH_DELETE);
+      *act = ACT_PERSIST;
+      return 1;
+    }
+    case PH_DELETE: {  // CompactorPhaseTwoDeleteLedger, :153-165
+      *act = ACT_DELETE;
+      const int m = k_max_ledger(L, k);
+      lkey u = lset(L, lset(L, k, L.ph_sh, 3, PH_ONE), L.p1r_sh, L.p1r_w, 0);
+      if (m != 1) {  // oldCompactedLedgerId = m - 1 (Nil when m = 1)
+        if (m - 1 < 1) return 2;  // compactedLedgers[old] out of domain
+        u = lset(L, u, led_base(L, m - 1), L.led_w, 0);
+      }
+      *t = u;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+// BrokerCrash, compaction.tla:169-182.  Returns 1 if enabled.
+TLCG_HD int crash_step_k(const Layout& L, lkey k, lkey* t) {
+  const int cr = k_crash(L, k);
+  if (cr >= L.K) return 0;
+  lkey u = lset(L, k, L.cr_sh, L.cr_w, (lkey)(cr + 1));
+  u = lset(L, u, L.ph_sh, 3, PH_ONE);
+  u = lset(L, u, L.p1r_sh, L.p1r_w, 0);
+  lkey h = 0, cc = 0;
+  if (k_cur_present(L, k)) {
+    h = (lkey)k_cur_h(L, k);
+    cc = (lkey)k_cur_c(L, k);
+  }
+  u = lset(L, u, L.hz_sh, L.hz_w, h);
+  *t = lset(L, u, L.ctx_sh, L.ctx_w, cc);
+  return 1;
+}
+
+// Consumer (:185-186) when modelled, and Terminating (:205-214)
+TLCG_HD int selfloop_count_k(const Layout& L, const CompMsgs& c, lkey k) {
+  const int term = c.len == L.N && L.term_ok && k_phase(L, k) == PH_WRITE && k_max_ledger(L, k) == L.C;
+  return (L.consumer ? 1 : 0) + term;
+}
+
+// ---- invariants on local keys ----
+
+// TypeSafe, compaction.tla:236-248 (model.h inv_typesafe)
+TLCG_HD int inv_typesafe_k(const Layout& L, const CompMsgs& c, lkey k) {
+  if (!c.msgs_ok) return EV_FALSE;
+  const int r = k_p1r(L, k);
+  if (r != 0 && r > c.len) return EV_FALSE;
+  if (k_phase(L, k) > PH_DELETE) return EV_FALSE;
+  if (k_hz(L, k) > L.N || k_ctx(L, k) > L.C || k_crash(L, k) > L.K) return EV_FALSE;
+  if (k_cur_present(L, k)) {
+    const int h = k_cur_h(L, k), cc = k_cur_c(L, k);
+    if (!(h >= 1 && h <= L.N && cc >= 1 && cc <= L.C)) return EV_FALSE;
+  }
+  return EV_TRUE;
+}
+
+// CompactedLedgerLeak, compaction.tla:253
+TLCG_HD int inv_leak_k(const Layout& L, lkey k) {
+  return popcount32(k & k_present_mask(L)) <= 2 ? EV_TRUE : EV_FALSE;
+}
+
+// CompactionHorizonCorrectness, compaction.tla:259-274 (model.h inv_horizon):
+// positions i = 1..hz in order; the first one that decides wins.
+TLCG_HD int inv_horizon_k(const Layout& L, const CompMsgs& c, lkey k) {
+  const int hz = k_hz(L, k);
+  if (hz == 0) return EV_TRUE;
+  const int upto = hz < c.len ? hz : c.len;  // positions with a message
+  const uint32_t live = (uint32_t)nmask(upto) & ~c.skip;
+  if (live) {
+    const int ctx = k_ctx(L, k);
+    // the first live position evaluates compactedLedgers[ctx]
+    if (ctx < 1 || ctx > L.C || !k_led_present(L, k, ctx)) return EV_ERROR;
+    const u64 m = k_led_mask(L, k, ctx);
+    for (int i = 0; i < L.N; ++i)
+      if (((live >> i) & 1) && !(m & ((c.need >> (i * L.N)) & nmask(L.N)))) return EV_FALSE;
+  }
+  return hz > c.len ? EV_ERROR : EV_TRUE;  // messages[len + 1] out of domain
+}
+
+// DuplicateNullKeyMessage, compaction.tla:280-294 (model.h inv_dupnull)
+TLCG_HD int inv_dupnull_k(const Layout& L, const CompMsgs& c, lkey k) {
+  const int ctx = k_ctx(L, k);
+  if (!(L.retain && ctx != 0)) return EV_TRUE;
+  if (ctx > L.C || !k_led_present(L, k, ctx)) return EV_ERROR;
+  const int hz = k_hz(L, k);
+  const u64 after = nmask(c.len < L.N ? c.len : L.N) & ~nmask(hz);
+  return ((u64)k_led_mask(L, k, ctx) & c.null_pos & after) ? EV_FALSE : EV_TRUE;
+}
+
+// first failing invariant in cfg order: -1 all hold, else (index << 1) | is_error
+TLCG_HD int check_invariants_k(const Layout& L, const CompMsgs& c, lkey k) {
+  for (int q = 0; q < L.n_inv; ++q) {
+    int r;
+    switch (L.inv[q]) {
+      case INV_TYPESAFE: r = inv_typesafe_k(L, c, k); break;
+      case INV_LEAK: r = inv_leak_k(L, k); break;
+      case INV_HORIZON: r = inv_horizon_k(L, c, k); break;
+      case INV_DUPNULL: r = inv_dupnull_k(L, c, k); break;
+      default: r = EV_ERROR;
+    }
+    if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
+  }
+  return -1;
+}
+
+}  // namespace tlcg

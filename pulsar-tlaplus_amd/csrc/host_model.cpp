@@ -2,10 +2,13 @@
 // model-level (context-free) C-ABI entry points.
 #include "host_model.h"
 
+#include "component_model.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <sstream>
+#include <unordered_set>
 
 namespace tlcg {
 
@@ -310,6 +313,50 @@ int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state) {
   std::string e;
   if (!m || !build_model(*m, &hm, &e)) return -2;
   return check_invariants(hm.L, state);
+}
+
+// Component-specialized evaluators (component_model.h) vs the generic ones
+// (model.h) on every state of the components of initial states
+// [first, first + n): the compactor successor, the stutter count and the
+// first failing invariant must agree.  Returns the states compared, or
+// -(1 + index of the first disagreeing state) on a mismatch.
+int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint64_t n) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e) || hm.L.producer) return -1;
+  const Layout& L = hm.L;
+  int64_t checked = 0;
+  const int mb = L.led_sh;
+  if (L.bits - mb > 32 || L.N > 8) return 0;  // the component engine does not take this model
+  for (u64 idx = first; idx < first + n && idx < hm.n_init; ++idx) {
+    const u64 s0 = init_state(L, idx);
+    const u64 msgs = s0 & L.msgs_mask;
+    const CompMsgs cm = comp_msgs_init(L, s0);
+    std::unordered_set<u64> seen{s0};
+    std::vector<u64> todo{s0};
+    while (!todo.empty()) {
+      const u64 s = todo.back();
+      todo.pop_back();
+      if ((s & L.msgs_mask) != msgs || (s >> mb) > 0xffffffffull) return -(1 + checked);
+      const lkey k = (lkey)(s >> mb);
+      u64 t1 = 0, t2w = 0;
+      lkey t2 = 0, c2 = 0;
+      int a1 = -1, a2 = -1;
+      const int r1 = compactor_step_ph(L, s, st_phase(L, s), &t1, &a1);
+      const int r2 = compactor_step_k(L, cm, msgs, k, k_phase(L, k), &t2, &a2);
+      const int x1 = crash_step(L, s, &t2w), x2 = crash_step_k(L, k, &c2);
+      if (r1 != r2 || a1 != a2 || (r1 == 1 && t1 != (msgs | ((u64)t2 << mb))) || x1 != x2 ||
+          (x1 && t2w != (msgs | ((u64)c2 << mb))) || check_invariants(L, s) != check_invariants_k(L, cm, k) ||
+          selfloop_count(L, s) != selfloop_count_k(L, cm, k))
+        return -(1 + checked);
+      ++checked;
+      u64 succ[64];
+      const int nsucc = host_successors(L, s, succ, nullptr, 64);
+      for (int i = 0; i < nsucc && i < 64; ++i)
+        if (seen.insert(succ[i]).second) todo.push_back(succ[i]);
+    }
+  }
+  return checked;
 }
 
 }  // extern "C"

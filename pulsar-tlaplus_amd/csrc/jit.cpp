@@ -37,6 +37,19 @@ std::string layout_literal(const Layout& L) {
 std::string program_source(const Layout& L) {
   std::string s = "typedef unsigned char uint8_t; typedef unsigned int uint32_t; typedef int int32_t;\n"
                   "typedef unsigned long uint64_t; typedef long int64_t;\n";
+  // tuning experiments: TLCG_JIT_DEFINES="A=1;B" becomes #define lines (part of the cache key)
+  if (const char* d = std::getenv("TLCG_JIT_DEFINES")) {
+    std::string all(d);
+    size_t i = 0;
+    while (i < all.size()) {
+      size_t j = all.find(';', i);
+      if (j == std::string::npos) j = all.size();
+      std::string kv = all.substr(i, j - i);
+      const size_t eq = kv.find('=');
+      if (!kv.empty()) s += "#define " + (eq == std::string::npos ? kv : kv.substr(0, eq) + " " + kv.substr(eq + 1)) + "\n";
+      i = j + 1;
+    }
+  }
   s += kJitSource;
   s += "\n" + layout_literal(L);
   for (int K : {32, 64, 128, 255})

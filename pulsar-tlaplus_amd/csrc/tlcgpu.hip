@@ -801,11 +801,13 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
 
 // ---- component engine (component.h) ----
 
-// applicable: `messages` immutable, one rank's components all local, local key fits 32 bits
+// applicable: `messages` immutable, one rank's components all local, local key fits 32 bits,
+// N <= 8 (component_model.h packs N x N bit masks)
 bool component_applicable(const tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   const int mb = L.msg_sh + L.N * L.mw;
-  return !L.producer && !c->opts.tlc_order && c->closed && L.bits - mb <= 32 && c->hm.n_init < (1ull << 36);
+  return !L.producer && !c->opts.tlc_order && c->closed && L.bits - mb <= 32 && L.N <= 8 &&
+         c->hm.n_init < (1ull << 36);
 }
 
 bool comp_scratch(tlcg_ctx* c, u64 n) {

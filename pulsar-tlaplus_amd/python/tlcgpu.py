@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_host_init_state": (U64, [M, U64]),
         "tlcg_host_successors": (C.c_int, [M, U64, C.POINTER(U64), C.POINTER(I32), I32]),
         "tlcg_host_check_invariants": (C.c_int, [M, U64]),
+        "tlcg_host_component_selfcheck": (C.c_int64, [M, U64, U64]),
         "tlcg_owner": (C.c_int, [P, U64]),
         "tlcg_expand": (C.c_int, [P, S]),
         "tlcg_outbox": (C.c_int, [P, I32, C.POINTER(P), C.POINTER(U64)]),
@@ -202,6 +203,13 @@ def host_successors(model: Model, state: int) -> List[Tuple[str, int]]:
     if n < 0:
         raise RuntimeError("evaluation error")
     return [(ACTIONS[acts[i]], out[i]) for i in range(n)]
+
+
+def host_component_selfcheck(model: Model, first: int, n: int) -> int:
+    """States on which the component engine's specialized evaluators were
+    compared with the generic ones (< 0: a disagreement)."""
+    m = model.to_c()
+    return load_library().tlcg_host_component_selfcheck(C.byref(m), C.c_uint64(first), C.c_uint64(n))
 
 
 def host_check_invariants(model: Model, state: int) -> int:

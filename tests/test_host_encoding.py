@@ -7,7 +7,7 @@ text byte for byte.  No GPU call is made."""
 import pytest
 
 import tlcgpu
-from conftest import GOLDEN, model_of
+from conftest import FULL_CASES, GOLDEN, model_of
 
 
 def host_bfs(m):
@@ -104,3 +104,14 @@ def test_phase_one_result_printing():
     (a, t), = [x for x in tlcgpu.host_successors(m, s) if x[0] == "CompactorPhaseOne"]
     txt = tlcgpu.decode(m, t)
     assert "phaseOneResult = [latestForKey |-> (2 :> 1 @@ 5 :> 2), readPosition |-> 3]" in txt
+
+
+@pytest.mark.parametrize("case", [c for c in FULL_CASES if not GOLDEN[c]["constants"]["producer"]])
+def test_component_specialization_matches_generic(case):
+    """component_model.h (messages-hoisted evaluators of the component engine)
+    agrees with model.h on every state of the first components of each
+    golden cfg: compactor successor, stutter count, first failing invariant."""
+    m = model_of(GOLDEN[case]["constants"])
+    n = tlcgpu.host_component_selfcheck(m, 0, 300)
+    bits = tlcgpu.load_library().tlcg_state_bits(m.to_c())
+    assert n > 0 or (n == 0 and bits > 32), n
