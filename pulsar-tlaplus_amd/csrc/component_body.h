@@ -72,19 +72,20 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       }
     }
     lvl_end = tail;
-    // visit one successor: FPSet lookup, insert, invariants (TLC's FPSet.put + check)
-    auto visit = [&](lkey key, int action, int pos) {
-      unsigned sl = slot_of<T>(key);
+    // visit one successor whose probe starts at slot `sl` holding `e`: FPSet
+    // lookup, insert, invariants (TLC's FPSet.put + check).  Returns the slot
+    // it inserted into, or -1.
+    auto visit = [&](lkey key, int action, int pos, unsigned sl, unsigned e) -> int {
       for (int p = 0; p < T; ++p) {
-        const unsigned e = h[sl][lane];
         if (e == 0) break;
-        if (q[e - 1][lane] == key) return;  // seen
+        if (q[e - 1][lane] == key) return -1;  // seen
         sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
+        e = h[sl][lane];
       }
       if (tail >= K) {  // does not fit on chip: cascade
         ovf = true;
         alive = false;
-        return;
+        return -1;
       }
       h[sl][lane] = (uint8_t)(tail + 1);
       q[tail][lane] = key;
@@ -98,9 +99,15 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
         lev = min(lev, make_comp_event(level + 1, idx0, pos, action, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
         alive = false;
       }
+      return (int)sl;
     };
+    // the state at the queue head lives in a register; the next one is read
+    // from LDS while this one expands
+    lkey cur = act ? (lkey)(s0 >> mb) : 0;
     while (alive && head < tail) {
-      const lkey s = q[head][lane];
+      const lkey s = cur;
+      const int tail0 = tail;
+      const lkey nxt = head + 1 < tail0 ? q[head + 1][lane] : 0;
       int nsucc = 0;
       lkey t = 0;
       int action = 0;
@@ -122,14 +129,23 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
         alive = false;
         break;
       }
+      lkey t2 = 0;
+      const bool crash = crash_step_k(L, s, &t2) != 0;  // BrokerCrash, compaction.tla:227
+      // both successors' first FPSet slots are read together
+      const unsigned sl1 = slot_of<T>(t), sl2 = slot_of<T>(t2);
+      const unsigned e1 = r == 1 ? h[sl1][lane] : 0;
+      unsigned e2 = crash ? h[sl2][lane] : 0;
+      lkey first_new = 0;
       if (r == 1) {
         ++nsucc;
-        visit(t, action, head);
+        const int ins = visit(t, action, head, sl1, e1);
+        if (ins >= 0) first_new = t;
+        if (ins == (int)sl2 && crash) e2 = h[sl2][lane];  // the slot just taken
       }
-      lkey t2 = 0;
-      if (alive && crash_step_k(L, s, &t2)) {  // BrokerCrash, compaction.tla:227
+      if (alive && crash) {
         ++nsucc;
-        visit(t2, ACT_CRASH, head);
+        const int ins = visit(t2, ACT_CRASH, head, sl2, e2);
+        if (ins >= 0 && tail0 == tail - 1) first_new = t2;
       }
       nsucc += selfloop_count_k(L, cmsg, s);  // Consumer / Terminating stutters
       lgen += (u64)nsucc;
@@ -139,6 +155,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       }
       if (!alive) break;
       ++head;
+      cur = head < tail0 ? nxt : first_new;  // position head was filled by this expansion
       if (head == lvl_end) {  // level `level` = [lvl_start, lvl_end) is complete
         if (level >= counted) atomicAdd(&lvl_sh[level], (unsigned)(lvl_end - lvl_start));
         ++level;
