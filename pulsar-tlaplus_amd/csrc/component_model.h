@@ -109,7 +109,7 @@ TLCG_HD int k_max_ledger(const Layout& L, lkey k) {
 
 // ---- Next disjuncts on local keys (model.h compactor_step_ph / crash_step) ----
 
-// The compactor disjunct, compaction.tla:93-165.  `full` rebuilds the whole
+// The compactor disjunct, compaction.tla:93-165.  `msgs` rebuilds the whole
 // word for the one case that needs more than the precomputed facts.
 // Returns 0 disabled, 1 enabled (*t, *act set), 2 evaluation error (*act set).
 TLCG_HD int compactor_step_k(const Layout& L, const CompMsgs& c, u64 msgs, lkey k, int ph, lkey* t, int* act) {
@@ -189,18 +189,14 @@ TLCG_HD int selfloop_count_k(const Layout& L, const CompMsgs& c, lkey k) {
 
 // ---- invariants on local keys ----
 
-// TypeSafe, compaction.tla:236-248 (model.h inv_typesafe)
+// TypeSafe, compaction.tla:236-248 (model.h inv_typesafe); one conjunction,
+// no early exits (TypeSafe has no evaluation-error cases)
 TLCG_HD int inv_typesafe_k(const Layout& L, const CompMsgs& c, lkey k) {
-  if (!c.msgs_ok) return EV_FALSE;
-  const int r = k_p1r(L, k);
-  if (r != 0 && r > c.len) return EV_FALSE;
-  if (k_phase(L, k) > PH_DELETE) return EV_FALSE;
-  if (k_hz(L, k) > L.N || k_ctx(L, k) > L.C || k_crash(L, k) > L.K) return EV_FALSE;
-  if (k_cur_present(L, k)) {
-    const int h = k_cur_h(L, k), cc = k_cur_c(L, k);
-    if (!(h >= 1 && h <= L.N && cc >= 1 && cc <= L.C)) return EV_FALSE;
-  }
-  return EV_TRUE;
+  const int r = k_p1r(L, k), h = k_cur_h(L, k), cc = k_cur_c(L, k);
+  const bool ok = c.msgs_ok & (r == 0 || r <= c.len) & (k_phase(L, k) <= PH_DELETE) & (k_hz(L, k) <= L.N) &
+                  (k_ctx(L, k) <= L.C) & (k_crash(L, k) <= L.K) &
+                  (!k_cur_present(L, k) || (h >= 1 && h <= L.N && cc >= 1 && cc <= L.C));
+  return ok ? EV_TRUE : EV_FALSE;
 }
 
 // CompactedLedgerLeak, compaction.tla:253
@@ -220,8 +216,9 @@ TLCG_HD int inv_horizon_k(const Layout& L, const CompMsgs& c, lkey k) {
     // the first live position evaluates compactedLedgers[ctx]
     if (ctx < 1 || ctx > L.C || !k_led_present(L, k, ctx)) return EV_ERROR;
     const u64 m = k_led_mask(L, k, ctx);
-    for (int i = 0; i < L.N; ++i)
-      if (((live >> i) & 1) && !(m & ((c.need >> (i * L.N)) & nmask(L.N)))) return EV_FALSE;
+    uint32_t fail = 0;  // live positions without a witness in the ledger
+    for (int i = 0; i < L.N; ++i) fail |= (uint32_t)((m & ((c.need >> (i * L.N)) & nmask(L.N))) == 0) << i;
+    if (fail & live) return EV_FALSE;
   }
   return hz > c.len ? EV_ERROR : EV_TRUE;  // messages[len + 1] out of domain
 }
