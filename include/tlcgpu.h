@@ -133,8 +133,12 @@ typedef struct tlcg_ctx tlcg_ctx;
 int tlcg_abi_version(void);
 /* ASSUME (compaction.tla:25-35) + packing check.  0 ok, <0 with a message in err. */
 int tlcg_check_model(const tlcg_model* m, char* err, int32_t cap);
-/* bits of the packed state word for these constants (<= 63 supported) */
+/* bits of the packed state for these constants (<= 126 supported) */
 int tlcg_state_bits(const tlcg_model* m);
+/* uint64 words per packed state: 1 (<= 63 bits) or 2 (a wide layout, <= 126
+ * bits).  Every entry point that passes a state as one uint64_t refuses wide
+ * layouts; its *_words twin takes `words` uint64s per state, low word first. */
+int tlcg_state_words(const tlcg_model* m);
 /* number of initial states (Init, compaction.tla:188-202) */
 uint64_t tlcg_init_count(const tlcg_model* m);
 
@@ -159,6 +163,10 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
 int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref);
 /* Copy stored states [first, first + n) to host memory. */
 int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out);
+/* the same for either width (states hold tlcg_state_words() uint64s each) */
+int tlcg_trace_words(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len);
+int tlcg_state_at_words(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref);
+int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out);
 /* Successor ordinal bits (to split a parent_ref). */
 int tlcg_ordinal_bits(const tlcg_model* m);
 int tlcg_action_of_ordinal(const tlcg_model* m, int32_t ordinal);
@@ -173,6 +181,12 @@ uint64_t tlcg_host_init_state(const tlcg_model* m, uint64_t idx);
 int tlcg_host_successors(const tlcg_model* m, uint64_t state, uint64_t* out, int32_t* actions, int32_t cap);
 /* First failing invariant of a state: -1 all hold, else (index << 1) | is_error. */
 int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state);
+/* the same for either width */
+int tlcg_decode_words(const tlcg_model* m, const uint64_t* state, char* buf, int32_t cap);
+int tlcg_host_init_state_words(const tlcg_model* m, uint64_t idx, uint64_t* out);
+int tlcg_host_successors_words(const tlcg_model* m, const uint64_t* state, uint64_t* out, int32_t* actions,
+                               int32_t cap);
+int tlcg_host_check_invariants_words(const tlcg_model* m, const uint64_t* state);
 /* Self-check of the component engine's specialized evaluators against the
  * generic ones on the components of initial states [first, first + n), host
  * only.  Returns the states compared (0: the component engine does not take

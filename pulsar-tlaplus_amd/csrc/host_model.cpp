@@ -75,9 +75,9 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
   L.ctx_sh = sh; L.ctx_w = bits_for((u64)L.C); sh += L.ctx_w;
   L.cr_sh = sh; L.cr_w = bits_for((u64)L.K); sh += L.cr_w;
   L.bits = sh;
-  if (L.bits > 63) {
+  if (L.bits > 126) {
     char b[160];
-    std::snprintf(b, sizeof b, "these constants need a %d-bit state; this build packs states into 63 bits", L.bits);
+    std::snprintf(b, sizeof b, "these constants need a %d-bit state; this build packs states into 126 bits", L.bits);
     return fail(b);
   }
   L.retain = m.retain_null_key ? 1 : 0;
@@ -90,9 +90,13 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
   L.ord_bits = bits_for((u64)(L.nkv + N_ACTIONS - 1));
   L.n_inv = m.n_invariants;
   for (int q = 0; q < m.n_invariants; ++q) L.inv[q] = m.invariants[q];
-  L.msgs_mask = (L.msg_sh + L.N * L.mw) >= 64 ? ~0ull : ((1ull << (L.msg_sh + L.N * L.mw)) - 1);
-  L.led_present_mask = 0;
-  for (int j = 1; j <= L.C; ++j) L.led_present_mask |= 1ull << led_base(L, j);
+  const u128 mm = wmask<u128>(L.msg_sh + L.N * L.mw);
+  L.msgs_mask = (u64)mm;
+  L.msgs_mask_hi = (u64)(mm >> 64);
+  u128 pm = 0;
+  for (int j = 1; j <= L.C; ++j) pm |= (u128)1 << led_base(L, j);
+  L.led_present_mask = (u64)pm;
+  L.led_present_mask_hi = (u64)(pm >> 64);
   // initial states
   if (L.producer) {
     hm.n_init = 1;
@@ -109,7 +113,8 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
   return true;
 }
 
-std::string format_state(const HostModel& hm, u64 s) {
+template <typename W>
+std::string format_state(const HostModel& hm, W s) {
   const Layout& L = hm.L;
   std::ostringstream o;
   int len = st_len(L, s);
@@ -179,7 +184,8 @@ std::string format_state(const HostModel& hm, u64 s) {
   return o.str();
 }
 
-int successor_at(const Layout& L, u64 s, int ord, u64* t) {
+template <typename W>
+int successor_at(const Layout& L, W s, int ord, W* t) {
   int act = action_of_ordinal(L, ord);
   if (act == ACT_PRODUCER) {
     if (!L.producer) return 0;
@@ -200,7 +206,7 @@ int successor_at(const Layout& L, u64 s, int ord, u64* t) {
     return 1;
   }
   int a2 = -1;
-  u64 u = 0;
+  W u = 0;
   int r = compactor_step(L, s, &u, &a2);
   if (r == 0 || a2 != act) return 0;
   if (r == 2) return 2;
@@ -208,9 +214,10 @@ int successor_at(const Layout& L, u64 s, int ord, u64* t) {
   return 1;
 }
 
-int host_successors(const Layout& L, u64 s, u64* out, int* actions, int cap) {
+template <typename W>
+int host_successors(const Layout& L, W s, W* out, int* actions, int cap) {
   int n = 0;
-  auto put = [&](u64 t, int a) {
+  auto put = [&](W t, int a) {
     if (n < cap) {
       out[n] = t;
       if (actions) actions[n] = a;
@@ -222,7 +229,7 @@ int host_successors(const Layout& L, u64 s, u64* out, int* actions, int cap) {
     if (len < L.N)
       for (int j = 0; j < L.nkv; ++j) put(producer_succ(L, s, len, j), ACT_PRODUCER);
   }
-  u64 t;
+  W t;
   int act;
   int r = compactor_step(L, s, &t, &act);
   if (r == 2) return -1;
@@ -232,6 +239,13 @@ int host_successors(const Layout& L, u64 s, u64* out, int* actions, int cap) {
   if (terminating_enabled(L, s)) put(s, ACT_TERMINATING);
   return n;
 }
+
+template std::string format_state<u64>(const HostModel&, u64);
+template std::string format_state<u128>(const HostModel&, u128);
+template int successor_at<u64>(const Layout&, u64, int, u64*);
+template int successor_at<u128>(const Layout&, u128, int, u128*);
+template int host_successors<u64>(const Layout&, u64, u64*, int*, int);
+template int host_successors<u128>(const Layout&, u128, u128*, int*, int);
 
 }  // namespace tlcg
 
@@ -281,37 +295,82 @@ int tlcg_action_of_ordinal(const tlcg_model* m, int32_t ordinal) {
   return action_of_ordinal(hm.L, ordinal);
 }
 
-int tlcg_decode(const tlcg_model* m, uint64_t state, char* buf, int32_t cap) {
+int tlcg_state_words(const tlcg_model* m) {
   HostModel hm;
   std::string e;
   if (!m || !build_model(*m, &hm, &e)) return -1;
-  std::string s = format_state(hm, state);
+  return state_words(hm.L);
+}
+
+int tlcg_decode_words(const tlcg_model* m, const uint64_t* state, char* buf, int32_t cap) {
+  HostModel hm;
+  std::string e;
+  if (!m || !state || !build_model(*m, &hm, &e)) return -1;
+  const int w = state_words(hm.L);
+  std::string s = w == 1 ? format_state<u64>(hm, state[0]) : format_state<u128>(hm, join_words(state, 2));
   if (buf && cap > 0) std::snprintf(buf, (size_t)cap, "%s", s.c_str());
   return (int)s.size();
 }
 
-uint64_t tlcg_host_init_state(const tlcg_model* m, uint64_t idx) {
+int tlcg_decode(const tlcg_model* m, uint64_t state, char* buf, int32_t cap) {
+  if (tlcg_state_words(m) != 1) return -2;  // wide layout: tlcg_decode_words
+  return tlcg_decode_words(m, &state, buf, cap);
+}
+
+int tlcg_host_init_state_words(const tlcg_model* m, uint64_t idx, uint64_t* out) {
   HostModel hm;
   std::string e;
-  if (!m || !build_model(*m, &hm, &e)) return ~0ull;
-  return init_state(hm.L, idx);
+  if (!m || !out || !build_model(*m, &hm, &e)) return -1;
+  split_words(init_state<u128>(hm.L, idx), out, state_words(hm.L));
+  return 0;
+}
+
+uint64_t tlcg_host_init_state(const tlcg_model* m, uint64_t idx) {
+  uint64_t w[2] = {~0ull, ~0ull};
+  if (tlcg_state_words(m) != 1 || tlcg_host_init_state_words(m, idx, w)) return ~0ull;
+  return w[0];
+}
+
+int tlcg_host_successors_words(const tlcg_model* m, const uint64_t* state, uint64_t* out, int32_t* actions,
+                               int32_t cap) {
+  HostModel hm;
+  std::string e;
+  if (!m || !state || !build_model(*m, &hm, &e)) return -2;
+  const int w = state_words(hm.L);
+  const int k = std::max(cap, 0);
+  std::vector<u128> succ((size_t)k);
+  std::vector<int> acts((size_t)k);
+  // the u128 instantiation computes the same successors as the u64 one for any layout
+  const int n = host_successors<u128>(hm.L, join_words(state, w), succ.data(), acts.data(), cap);
+  for (int i = 0; i < std::min(n, (int)cap); ++i) {
+    if (out) split_words(succ[(size_t)i], out + (size_t)i * w, w);
+    if (actions) actions[i] = acts[(size_t)i];
+  }
+  return n;
 }
 
 int tlcg_host_successors(const tlcg_model* m, uint64_t state, uint64_t* out, int32_t* actions, int32_t cap) {
   HostModel hm;
   std::string e;
-  if (!m || !build_model(*m, &hm, &e)) return -2;
+  if (!m || !build_model(*m, &hm, &e) || state_words(hm.L) != 1) return -2;
   std::vector<int> acts((size_t)std::max(cap, 0));
-  int n = host_successors(hm.L, state, out, acts.data(), cap);
+  int n = host_successors<u64>(hm.L, state, out, acts.data(), cap);
   if (actions)
     for (int i = 0; i < std::min(n, (int)cap); ++i) actions[i] = acts[(size_t)i];
   return n;
 }
 
+int tlcg_host_check_invariants_words(const tlcg_model* m, const uint64_t* state) {
+  HostModel hm;
+  std::string e;
+  if (!m || !state || !build_model(*m, &hm, &e)) return -2;
+  return check_invariants<u128>(hm.L, join_words(state, state_words(hm.L)));
+}
+
 int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state) {
   HostModel hm;
   std::string e;
-  if (!m || !build_model(*m, &hm, &e)) return -2;
+  if (!m || !build_model(*m, &hm, &e) || state_words(hm.L) != 1) return -2;
   return check_invariants(hm.L, state);
 }
 

@@ -22,12 +22,23 @@ struct HostModel {
 bool build_model(const tlcg_model& m, HostModel* out, std::string* err);
 
 // TLC value syntax of a packed state (compaction.tla:57-70 declaration order).
-std::string format_state(const HostModel& hm, u64 s);
+template <typename W>
+std::string format_state(const HostModel& hm, W s);
 
 // Successor of `s` at Next ordinal `ord`; returns 1 ok, 0 disabled, 2 eval error.
-int successor_at(const Layout& L, u64 s, int ord, u64* t);
+template <typename W>
+int successor_at(const Layout& L, W s, int ord, W* t);
 
 // All successors in Next order; returns count or -1 on an evaluation error.
-int host_successors(const Layout& L, u64 s, u64* out, int* actions, int cap);
+template <typename W>
+int host_successors(const Layout& L, W s, W* out, int* actions, int cap);
+
+// words of the packed state: 1 (<= 63 bits) or 2 (wide layouts, <= 126 bits)
+inline int state_words(const Layout& L) { return L.bits <= 63 ? 1 : 2; }
+inline u128 join_words(const uint64_t* w, int n) { return n == 1 ? (u128)w[0] : ((u128)w[0] | ((u128)w[1] << 64)); }
+inline void split_words(u128 s, uint64_t* w, int n) {
+  w[0] = (uint64_t)s;
+  if (n > 1) w[1] = (uint64_t)(s >> 64);
+}
 
 }  // namespace tlcg

@@ -21,7 +21,7 @@ constexpr u64 NO_PARENT = ~0ull;
 // event kinds (an event stops the run, like TLC's first error)
 enum EventKind { EVK_VIOLATION = 0, EVK_INV_ERROR = 1, EVK_DEADLOCK = 2, EVK_ACTION_ERROR = 3 };
 // overflow flags
-enum Overflow { OVF_FPSET = 1, OVF_STORE = 2, OVF_OUTBOX = 4, OVF_DUP_INIT = 8 };
+enum Overflow { OVF_FPSET = 1, OVF_STORE = 2, OVF_OUTBOX = 4, OVF_DUP_INIT = 8, OVF_WIDE_SPIN = 16 };
 
 // per-level counter block, zeroed (event = ~0) before every level
 struct LevelCtr {
@@ -43,23 +43,88 @@ TLCG_HD u64 make_event(u64 dkey, int kind, int index) {
 // holds 0 (empty) or state|SLOT_TAG.  Slots only ever go 0 -> key, so a plain
 // (possibly stale) load that sees a key is exact, and a stale 0 is resolved by
 // the device-scope CAS.  Returns 1 inserted, 0 present, -1 probe limit.
-__device__ __forceinline__ int fpset_put(u64* __restrict__ slots, int log2, u64 state, u64 fp,
-                                         u64* slot_out) {
-  const u64 key = state | SLOT_TAG;
+//
+// Wide states (u128, <= 126 bits): 16-byte slots {hi, lo}.  hi carries the
+// state's bits 64..125 | SLOT_TAG, and WIDE_READY once lo is published.  An
+// insert claims hi with a 64-bit CAS (0 -> hi), publishes lo with an atomic
+// exchange, waits for it, then sets WIDE_READY; a prober whose hi matches waits
+// for WIDE_READY and compares lo.  Every access after the claim is a
+// device-scope atomic, performed at the memory side, so no XCD's L2 can serve a
+// stale half.  Slots only go 0 -> hi -> hi|READY, so a stale plain first load
+// is harmless (0 -> the CAS decides; hi without READY -> the wait re-reads).
+constexpr u64 WIDE_READY = 1ull << 62;
+constexpr int WIDE_SPIN = 1 << 22;  // bound on the wait for a publisher (then OVF_WIDE_SPIN)
+
+template <typename W>
+__device__ __forceinline__ int fpset_put(u64* __restrict__ slots, int log2, W state, u64 fp, u64* slot_out) {
   const u64 mask = (1ull << log2) - 1;
   u64 i = fp >> (64 - log2);
+  if constexpr (sizeof(W) == 8) {
+    const u64 key = state | SLOT_TAG;
 #pragma unroll 1
-  for (int p = 0; p < MAX_PROBE; ++p) {
-    u64 v = __builtin_nontemporal_load(&slots[i]);
-    if (v == key) { *slot_out = i; return 0; }
-    if (v == 0) {
-      u64 old = atomicCAS((unsigned long long*)&slots[i], 0ull, (unsigned long long)key);
-      if (old == 0) { *slot_out = i; return 1; }
-      if (old == key) { *slot_out = i; return 0; }
+    for (int p = 0; p < MAX_PROBE; ++p) {
+      u64 v = __builtin_nontemporal_load(&slots[i]);
+      if (v == key) { *slot_out = i; return 0; }
+      if (v == 0) {
+        u64 old = atomicCAS((unsigned long long*)&slots[i], 0ull, (unsigned long long)key);
+        if (old == 0) { *slot_out = i; return 1; }
+        if (old == key) { *slot_out = i; return 0; }
+      }
+      i = (i + 1) & mask;
     }
-    i = (i + 1) & mask;
+    return -1;
+  } else {
+    // The probe is a wave-uniform loop (it runs while ANY lane is unsettled)
+    // so that a lane waiting on a slot that another lane of its own wave has
+    // just claimed cannot spin ahead of that lane's publish: both happen in
+    // the same trip.
+    const u64 hi = (u64)(state >> 64) | SLOT_TAG, lo = (u64)state;
+    enum { PROBING, CLAIMED, WAITING, SETTLED };
+    int st = PROBING, res = -1, probes = 0, spins = 0;
+    while (__any(st != SETTLED)) {
+      unsigned long long* sl = (unsigned long long*)&slots[2 * i];
+      if (st == PROBING) {
+        u64 v = __builtin_nontemporal_load(&slots[2 * i]);
+        if (v == 0) {
+          v = atomicCAS(&sl[0], 0ull, (unsigned long long)hi);
+          if (v == 0) st = CLAIMED;
+        }
+        if (st == PROBING) {
+          if ((v & ~WIDE_READY) == hi) {
+            st = WAITING;  // the same high half: compare the low half once published
+          } else if (++probes >= MAX_PROBE) {
+            st = SETTLED;
+          } else {
+            i = (i + 1) & mask;
+          }
+        }
+      }
+      if (st == CLAIMED) {  // publish lo, wait for it, then mark the slot ready
+        atomicExch(&sl[1], (unsigned long long)lo);
+        __builtin_amdgcn_s_waitcnt(0);
+        atomicOr(&sl[0], (unsigned long long)WIDE_READY);
+        st = SETTLED;
+        res = 1;
+      } else if (st == WAITING) {
+        if (atomicOr(&sl[0], 0ull) & WIDE_READY) {
+          if (atomicOr(&sl[1], 0ull) == lo) {
+            st = SETTLED;
+            res = 0;
+          } else if (++probes >= MAX_PROBE) {
+            st = SETTLED;
+          } else {
+            st = PROBING;
+            i = (i + 1) & mask;
+          }
+        } else if (++spins >= WIDE_SPIN) {
+          st = SETTLED;
+          res = -2;
+        }
+      }
+    }
+    *slot_out = i;
+    return res;
   }
-  return -1;
 }
 
 // continue an insert from slot i (the slots before it on the probe path are
@@ -86,8 +151,8 @@ __device__ __forceinline__ u64 lanemask_lt() {
 
 // Wave-aggregated append into the block's LDS stage.  Must be reached by all
 // lanes of the wave (uniform control flow).
-template <bool WITH_SLOT>
-__device__ __forceinline__ void stage_append(bool pred, u64 st, u64 par, u64 slot, u64* s_st, u64* s_par,
+template <bool WITH_SLOT, typename W>
+__device__ __forceinline__ void stage_append(bool pred, W st, u64 par, u64 slot, W* s_st, u64* s_par,
                                              u64* s_slot, unsigned* s_cnt) {
   const u64 m = __ballot(pred);
   if (m == 0) return;
@@ -102,27 +167,6 @@ __device__ __forceinline__ void stage_append(bool pred, u64 st, u64 par, u64 slo
     if (WITH_SLOT) s_slot[pos] = slot;
   }
 }
-
-// arguments of one BFS level's expansion (the global engine)
-struct ExpandArgs {
-  Layout L;
-  const u64* frontier;
-  u64 n_front;
-  u64 front_gidx0;  // gidx of frontier[0]
-  u64* slots;
-  int log2;
-  u64* states_out;  // next level (store + level_base[d+1])
-  u64* parents_out;
-  u64 cap_out;      // room for new states
-  u64* slot_out;    // TLC order: FPSet slot of every new state
-  u64* dkey_slot;   // TLC order: min discovery key per FPSet slot
-  LevelCtr* ctr;
-  u64 rank_tag;     // rank << 56
-  int rank, world;
-  u64 owner_mask;
-  u64* outbox;      // world > 1: [world][outbox_cap] records {state, parent_ref}
-  u64 outbox_cap;
-};
 
 __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
 #pragma unroll

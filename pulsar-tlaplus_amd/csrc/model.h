@@ -31,6 +31,11 @@
 // Every state of the reachable space encodes to exactly one word (canonical),
 // so equality of words == equality of TLC states, and the FPSet can store the
 // word itself: dedup is exact (no fingerprint collisions).
+//
+// The word type W is a template parameter: u64 for layouts of <= 63 bits
+// (every kernel's fast path), u128 for wider ones (up to 126 bits, e.g.
+// CompactionTimesLimit = 12; the wide engine, wide.hip).  Field values
+// themselves always fit 64 bits.
 #pragma once
 #if defined(__HIPCC_RTC__)
 // compiled at run time by hipRTC (jit.cpp): the runtime headers are built in
@@ -48,6 +53,7 @@
 namespace tlcg {
 
 typedef uint64_t u64;
+typedef unsigned __int128 u128;
 
 // compaction.tla:39-44 (declaration order)
 enum Phase { PH_ONE = 0, PH_WRITE, PH_UCTX, PH_UHOR, PH_PERSIST, PH_DELETE };
@@ -75,13 +81,16 @@ struct Layout {
   int32_t hz_sh, hz_w;
   int32_t ctx_sh, ctx_w;
   int32_t cr_sh, cr_w;
-  int32_t bits;                // total state bits (<= 63: bit 63 tags FPSet slots)
+  int32_t bits;                // total state bits (<= 63: one u64 word, bit 63 tags FPSet slots;
+                               // <= 126: two words, wide.hip)
   int32_t retain, producer, consumer, term_ok, check_deadlock;
   int32_t ord_bits;            // bits of a successor ordinal (Next position)
   int32_t n_inv;
   int32_t inv[8];              // invariant kinds in cfg order (compaction.cfg:25-31)
-  u64 msgs_mask;               // bits holding `messages`
-  u64 led_present_mask;        // bit0 of every ledger slot
+  u64 msgs_mask;               // bits holding `messages` (low word)
+  u64 led_present_mask;        // bit0 of every ledger slot (low word)
+  u64 msgs_mask_hi;            // the same masks' bits 64..127 (wide layouts)
+  u64 led_present_mask_hi;
 };
 
 TLCG_HD int bits_for(u64 maxval) {  // bits to represent 0..maxval
@@ -90,12 +99,34 @@ TLCG_HD int bits_for(u64 maxval) {  // bits to represent 0..maxval
   return b;
 }
 
-TLCG_HD u64 fget(u64 s, int sh, int w) { return w ? (s >> sh) & ((~0ull) >> (64 - w)) : 0; }
-TLCG_HD u64 fset(u64 s, int sh, int w, u64 v) {
-  if (!w) return s;
-  u64 m = ((~0ull) >> (64 - w)) << sh;
-  return (s & ~m) | ((v << sh) & m);
+template <typename W>
+TLCG_HD W wmask(int w) {
+  return w >= (int)(8 * sizeof(W)) ? ~(W)0 : (((W)1 << w) - 1);
 }
+template <typename W>
+TLCG_HD u64 fget(W s, int sh, int w) {
+  return w ? (u64)((s >> sh) & wmask<W>(w)) : 0;
+}
+template <typename W>
+TLCG_HD W fset(W s, int sh, int w, u64 v) {
+  if (!w) return s;
+  const W m = wmask<W>(w) << sh;
+  return (s & ~m) | (((W)v << sh) & m);
+}
+// a Layout mask (low and high halves) as a W
+template <typename W>
+TLCG_HD W wide_mask(u64 lo, u64 hi) {
+  if constexpr (sizeof(W) == 8) {
+    (void)hi;
+    return lo;
+  } else {
+    return (W)lo | ((W)hi << 64);
+  }
+}
+template <typename W>
+TLCG_HD W present_mask(const Layout& L) { return wide_mask<W>(L.led_present_mask, L.led_present_mask_hi); }
+template <typename W>
+TLCG_HD W messages_mask(const Layout& L) { return wide_mask<W>(L.msgs_mask, L.msgs_mask_hi); }
 
 // murmur3 fmix64: a bijection on 64-bit words.  The "fingerprint" of a state
 // is mix64(word); since the word is canonical and mix64 invertible, distinct
@@ -108,20 +139,20 @@ TLCG_HD u64 mix64(u64 x) {
 }
 
 // ---- field accessors ----
-TLCG_HD int st_len(const Layout& L, u64 s) { return (int)fget(s, L.len_sh, L.len_w); }
-TLCG_HD int st_key(const Layout& L, u64 s, int pos1) { return (int)fget(s, L.msg_sh + (pos1 - 1) * L.mw, L.kb); }
-TLCG_HD int st_val(const Layout& L, u64 s, int pos1) { return (int)fget(s, L.msg_sh + (pos1 - 1) * L.mw + L.kb, L.vb); }
-TLCG_HD int st_phase(const Layout& L, u64 s) { return (int)fget(s, L.ph_sh, 3); }
-TLCG_HD int st_p1r(const Layout& L, u64 s) { return (int)fget(s, L.p1r_sh, L.p1r_w); }
-TLCG_HD int st_hz(const Layout& L, u64 s) { return (int)fget(s, L.hz_sh, L.hz_w); }
-TLCG_HD int st_ctx(const Layout& L, u64 s) { return (int)fget(s, L.ctx_sh, L.ctx_w); }
-TLCG_HD int st_crash(const Layout& L, u64 s) { return (int)fget(s, L.cr_sh, L.cr_w); }
+template <typename W> TLCG_HD int st_len(const Layout& L, W s) { return (int)fget(s, L.len_sh, L.len_w); }
+template <typename W> TLCG_HD int st_key(const Layout& L, W s, int pos1) { return (int)fget(s, L.msg_sh + (pos1 - 1) * L.mw, L.kb); }
+template <typename W> TLCG_HD int st_val(const Layout& L, W s, int pos1) { return (int)fget(s, L.msg_sh + (pos1 - 1) * L.mw + L.kb, L.vb); }
+template <typename W> TLCG_HD int st_phase(const Layout& L, W s) { return (int)fget(s, L.ph_sh, 3); }
+template <typename W> TLCG_HD int st_p1r(const Layout& L, W s) { return (int)fget(s, L.p1r_sh, L.p1r_w); }
+template <typename W> TLCG_HD int st_hz(const Layout& L, W s) { return (int)fget(s, L.hz_sh, L.hz_w); }
+template <typename W> TLCG_HD int st_ctx(const Layout& L, W s) { return (int)fget(s, L.ctx_sh, L.ctx_w); }
+template <typename W> TLCG_HD int st_crash(const Layout& L, W s) { return (int)fget(s, L.cr_sh, L.cr_w); }
 TLCG_HD int led_base(const Layout& L, int j1) { return L.led_sh + (j1 - 1) * L.led_w; }
-TLCG_HD int led_present(const Layout& L, u64 s, int j1) { return (int)((s >> led_base(L, j1)) & 1); }
-TLCG_HD u64 led_mask(const Layout& L, u64 s, int j1) { return fget(s, led_base(L, j1) + 1, L.N); }
-TLCG_HD int cur_present(const Layout& L, u64 s) { return (int)((s >> L.cur_sh) & 1); }
-TLCG_HD int cur_h(const Layout& L, u64 s) { return (int)fget(s, L.cur_sh + 1, L.curh_w); }
-TLCG_HD int cur_c(const Layout& L, u64 s) { return (int)fget(s, L.cur_sh + 1 + L.curh_w, L.curc_w); }
+template <typename W> TLCG_HD int led_present(const Layout& L, W s, int j1) { return (int)((s >> led_base(L, j1)) & 1); }
+template <typename W> TLCG_HD u64 led_mask(const Layout& L, W s, int j1) { return fget(s, led_base(L, j1) + 1, L.N); }
+template <typename W> TLCG_HD int cur_present(const Layout& L, W s) { return (int)((s >> L.cur_sh) & 1); }
+template <typename W> TLCG_HD int cur_h(const Layout& L, W s) { return (int)fget(s, L.cur_sh + 1, L.curh_w); }
+template <typename W> TLCG_HD int cur_c(const Layout& L, W s) { return (int)fget(s, L.cur_sh + 1 + L.curh_w, L.curc_w); }
 
 TLCG_HD int popcount64(u64 x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -138,18 +169,43 @@ TLCG_HD int highbit64(u64 x) {  // index of the highest set bit, x != 0
 #endif
 }
 
+template <typename W>
+TLCG_HD int highbit(W x) {  // x != 0
+  if constexpr (sizeof(W) == 8) {
+    return highbit64(x);
+  } else {
+    const u64 hi = (u64)(x >> 64);
+    return hi ? 64 + highbit64(hi) : highbit64((u64)x);
+  }
+}
+template <typename W>
+TLCG_HD int popcount(W x) {
+  if constexpr (sizeof(W) == 8) return popcount64(x);
+  else return popcount64((u64)x) + popcount64((u64)(x >> 64));
+}
+// slot hash of a state: mix64 (a bijection) of a one-word state; for a wide
+// state a mix of both halves (the wide FPSet stores the whole state, so the
+// hash only spreads, it never decides equality)
+template <typename W>
+TLCG_HD u64 mixw(W s) {
+  if constexpr (sizeof(W) == 8) return mix64(s);
+  else return mix64((u64)s ^ mix64((u64)(s >> 64) + 0x9E3779B97F4A7C15ull));
+}
+
 // MaxCompactedLedgerId, compaction.tla:103-106
-TLCG_HD int max_ledger(const Layout& L, u64 s) {
-  u64 p = s & L.led_present_mask;
+template <typename W>
+TLCG_HD int max_ledger(const Layout& L, W s) {
+  const W p = s & present_mask<W>(L);
   if (!p) return 0;
-  return (highbit64(p) - L.led_sh) / L.led_w + 1;
+  return (highbit<W>(p) - L.led_sh) / L.led_w + 1;
 }
 
 // CompactMessages(messages, phaseOneResult) as a position mask over 1..r,
 // compaction.tla:107-119: keep position i iff it is the last occurrence of its
 // key in 1..r (i = latestForKey[key], :98 with Max :91), or its key is NullKey
 // and RetainNullKey.  Walk r..1 remembering the keys already seen.
-TLCG_HD u64 compact_mask(const Layout& L, u64 s, int r) {
+template <typename W>
+TLCG_HD u64 compact_mask(const Layout& L, W s, int r) {
   u64 seen = 0, mask = 0;
   for (int i = r; i >= 1; --i) {
     int k = st_key(L, s, i);
@@ -166,9 +222,10 @@ TLCG_HD u64 compact_mask(const Layout& L, u64 s, int r) {
 // Initial state number `idx` in TLC's Init enumeration (compaction.tla:188-202):
 // messages \in {msgs \in [1..N -> [id, key, value]] : msgs[i].id = i}; message 1
 // varies fastest, key faster than value ([TLC-ext] enumeration order).
-TLCG_HD u64 init_state(const Layout& L, u64 idx) {
+template <typename W = u64>
+TLCG_HD W init_state(const Layout& L, u64 idx) {
   if (L.producer) return 0;  // messages = <<>>, everything else Nil/0/PhaseOne
-  u64 s = fset(0, L.len_sh, L.len_w, (u64)L.N);
+  W s = fset((W)0, L.len_sh, L.len_w, (u64)L.N);
   for (int i = 1; i <= L.N; ++i) {
     u64 d = idx % (u64)L.nkv;
     idx /= (u64)L.nkv;
@@ -189,22 +246,24 @@ TLCG_HD int action_of_ordinal(const Layout& L, int ord) {
 
 // Producer, compaction.tla:83-87: successor number j (key index j / nv,
 // value index j % nv; key outer, value inner).  Caller checks len < N.
-TLCG_HD u64 producer_succ(const Layout& L, u64 s, int len, int j) {
+template <typename W>
+TLCG_HD W producer_succ(const Layout& L, W s, int len, int j) {
   u64 k = (u64)(j / L.nv), v = (u64)(j % L.nv);
-  u64 t = fset(s, L.msg_sh + len * L.mw, L.mw, k | (v << L.kb));
+  W t = fset(s, L.msg_sh + len * L.mw, L.mw, k | (v << L.kb));
   return fset(t, L.len_sh, L.len_w, (u64)(len + 1));
 }
 
 // The six compactor disjuncts (compaction.tla:93-165) are mutually exclusive
 // on compactorState, so a state has at most one compactor successor.
 // Returns 0 disabled, 1 enabled (*t, *act set), 2 evaluation error (*act set).
-TLCG_HD int compactor_step_ph(const Layout& L, u64 s, int ph, u64* t, int* act) {
+template <typename W>
+TLCG_HD int compactor_step_ph(const Layout& L, W s, int ph, W* t, int* act) {
   int p1r = st_p1r(L, s);
   switch (ph) {
     case PH_ONE: {  // CompactorPhaseOne, :93-100
       int len = st_len(L, s);
       if (p1r != 0 || len <= 0) return 0;
-      u64 u = fset(s, L.p1r_sh, L.p1r_w, (u64)len);
+      W u = fset(s, L.p1r_sh, L.p1r_w, (u64)len);
       *t = fset(u, L.ph_sh, 3, PH_WRITE);
       *act = ACT_PHASEONE;
       return 1;
@@ -214,13 +273,13 @@ TLCG_HD int compactor_step_ph(const Layout& L, u64 s, int ph, u64* t, int* act) 
       int nid = max_ledger(L, s) + 1;
       if (nid > L.C) return 0;  // newCompactedLedgerId \in 1..CompactionTimesLimit
       u64 mask = compact_mask(L, s, p1r);
-      u64 u = fset(s, led_base(L, nid), L.led_w, 1ull | (mask << 1));
+      W u = fset(s, led_base(L, nid), L.led_w, 1ull | (mask << 1));
       *t = fset(u, L.ph_sh, 3, PH_UCTX);
       *act = ACT_WRITE;
       return 1;
     }
     case PH_UCTX: {  // CompactorPhaseTwoUpdateContext, :135-139
-      u64 u = fset(s, L.ctx_sh, L.ctx_w, (u64)max_ledger(L, s));
+      W u = fset(s, L.ctx_sh, L.ctx_w, (u64)max_ledger(L, s));
       *t = fset(u, L.ph_sh, 3, PH_UHOR);
       *act = ACT_UCTX;
       return 1;
@@ -228,13 +287,13 @@ TLCG_HD int compactor_step_ph(const Layout& L, u64 s, int ph, u64* t, int* act) 
     case PH_UHOR: {  // CompactorPhaseTwoUpdateHorizon, :141-145
       *act = ACT_UHOR;
       if (p1r == 0) return 2;  // phaseOneResult.readPosition of Nil
-      u64 u = fset(s, L.hz_sh, L.hz_w, (u64)p1r);
+      W u = fset(s, L.hz_sh, L.hz_w, (u64)p1r);
       *t = fset(u, L.ph_sh, 3, PH_PERSIST);
       return 1;
     }
     case PH_PERSIST: {  // CompactorPhaseTwoPersistCusror, :147-151
       u64 cur = 1ull | ((u64)st_hz(L, s) << 1) | ((u64)st_ctx(L, s) << (1 + L.curh_w));
-      u64 u = fset(s, L.cur_sh, 1 + L.curh_w + L.curc_w, cur);
+      W u = fset(s, L.cur_sh, 1 + L.curh_w + L.curc_w, cur);
       *t = fset(u, L.ph_sh, 3, PH_DELETE);
       *act = ACT_PERSIST;
       return 1;
@@ -242,7 +301,7 @@ TLCG_HD int compactor_step_ph(const Layout& L, u64 s, int ph, u64* t, int* act) 
     case PH_DELETE: {  // CompactorPhaseTwoDeleteLedger, :153-165
       *act = ACT_DELETE;
       int m = max_ledger(L, s);
-      u64 u = fset(s, L.ph_sh, 3, PH_ONE);
+      W u = fset(s, L.ph_sh, 3, PH_ONE);
       u = fset(u, L.p1r_sh, L.p1r_w, 0);
       if (m != 1) {  // oldCompactedLedgerId = m - 1 (Nil when m = 1)
         int old = m - 1;
@@ -256,15 +315,17 @@ TLCG_HD int compactor_step_ph(const Layout& L, u64 s, int ph, u64* t, int* act) 
   return 0;
 }
 
-TLCG_HD int compactor_step(const Layout& L, u64 s, u64* t, int* act) {
+template <typename W>
+TLCG_HD int compactor_step(const Layout& L, W s, W* t, int* act) {
   return compactor_step_ph(L, s, st_phase(L, s), t, act);
 }
 
 // BrokerCrash, compaction.tla:169-182.  Returns 1 if enabled.
-TLCG_HD int crash_step(const Layout& L, u64 s, u64* t) {
+template <typename W>
+TLCG_HD int crash_step(const Layout& L, W s, W* t) {
   int cr = st_crash(L, s);
   if (cr >= L.K) return 0;
-  u64 u = fset(s, L.cr_sh, L.cr_w, (u64)(cr + 1));
+  W u = fset(s, L.cr_sh, L.cr_w, (u64)(cr + 1));
   u = fset(u, L.ph_sh, 3, PH_ONE);
   u = fset(u, L.p1r_sh, L.p1r_w, 0);
   u64 h = 0, c = 0;
@@ -275,20 +336,23 @@ TLCG_HD int crash_step(const Layout& L, u64 s, u64* t) {
 }
 
 // Terminating, compaction.tla:205-214 (consumeTimes is the constant 0).
-TLCG_HD int terminating_enabled(const Layout& L, u64 s) {
+template <typename W>
+TLCG_HD int terminating_enabled(const Layout& L, W s) {
   return st_len(L, s) == L.N && st_phase(L, s) == PH_WRITE && max_ledger(L, s) == L.C && L.term_ok;
 }
 
 // Stuttering successors (Consumer :185-186 when ModelConsumer; Terminating).
 // They equal the parent, so they are generated but never new.
-TLCG_HD int selfloop_count(const Layout& L, u64 s) {
+template <typename W>
+TLCG_HD int selfloop_count(const Layout& L, W s) {
   return (L.consumer ? 1 : 0) + terminating_enabled(L, s);
 }
 
 // ---- invariants ----
 
 // TypeSafe, compaction.tla:236-248
-TLCG_HD int inv_typesafe(const Layout& L, u64 s) {
+template <typename W>
+TLCG_HD int inv_typesafe(const Layout& L, W s) {
   int len = st_len(L, s);
   if (len > L.N) return EV_FALSE;
   for (int i = 1; i <= len; ++i)
@@ -305,14 +369,16 @@ TLCG_HD int inv_typesafe(const Layout& L, u64 s) {
 }
 
 // CompactedLedgerLeak, compaction.tla:253
-TLCG_HD int inv_leak(const Layout& L, u64 s) {
-  return popcount64(s & L.led_present_mask) <= 2 ? EV_TRUE : EV_FALSE;
+template <typename W>
+TLCG_HD int inv_leak(const Layout& L, W s) {
+  return popcount<W>(s & present_mask<W>(L)) <= 2 ? EV_TRUE : EV_FALSE;
 }
 
 // CompactionHorizonCorrectness, compaction.tla:259-274.  The LET-bound
 // compactedLedgers[compactedTopicContext] is only evaluated (and can only
 // fail) for an i that reaches it, in TLC's left-to-right order.
-TLCG_HD int inv_horizon(const Layout& L, u64 s) {
+template <typename W>
+TLCG_HD int inv_horizon(const Layout& L, W s) {
   int hz = st_hz(L, s), len = st_len(L, s), ctx = st_ctx(L, s);
   for (int i = 1; i <= hz; ++i) {
     if (i > len) return EV_ERROR;  // messages[i] out of domain
@@ -336,7 +402,8 @@ TLCG_HD int inv_horizon(const Layout& L, u64 s) {
 
 // DuplicateNullKeyMessage, compaction.tla:280-294: a null-key entry of
 // ledger[context] must not equal a message after the horizon.
-TLCG_HD int inv_dupnull(const Layout& L, u64 s) {
+template <typename W>
+TLCG_HD int inv_dupnull(const Layout& L, W s) {
   int ctx = st_ctx(L, s);
   if (!(L.retain && ctx != 0)) return EV_TRUE;
   if (ctx > L.C || !led_present(L, s, ctx)) return EV_ERROR;
@@ -347,7 +414,8 @@ TLCG_HD int inv_dupnull(const Layout& L, u64 s) {
   return EV_TRUE;
 }
 
-TLCG_HD int eval_invariant(const Layout& L, int kind, u64 s) {
+template <typename W>
+TLCG_HD int eval_invariant(const Layout& L, int kind, W s) {
   switch (kind) {
     case INV_TYPESAFE: return inv_typesafe(L, s);
     case INV_LEAK: return inv_leak(L, s);
@@ -359,7 +427,8 @@ TLCG_HD int eval_invariant(const Layout& L, int kind, u64 s) {
 
 // First failing invariant in cfg order: returns -1 if all hold, else
 // (index << 1) | is_error.
-TLCG_HD int check_invariants(const Layout& L, u64 s) {
+template <typename W>
+TLCG_HD int check_invariants(const Layout& L, W s) {
   for (int q = 0; q < L.n_inv; ++q) {
     int r = eval_invariant(L, L.inv[q], s);
     if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);

@@ -48,21 +48,28 @@ struct ExpandArgs {
   u64 outbox_cap;
 };
 
-__device__ __forceinline__ int owner_of(u64 s, u64 owner_mask, int world) {
-  return (int)(((mix64(s & owner_mask) >> 32) * (u64)world) >> 32);
+// owner rank of a state: wide states are only partitioned by `messages`,
+// which then lies in the low word (tlcg_create checks)
+template <typename W>
+__device__ __forceinline__ int owner_of(W s, u64 owner_mask, int world) {
+  return (int)(((mix64((u64)s & owner_mask) >> 32) * (u64)world) >> 32);
 }
+
+// overflow flag of a failed FPSet insert
+__device__ __forceinline__ unsigned ovf_of(int r) { return r == -2 ? (unsigned)OVF_WIDE_SPIN : (unsigned)OVF_FPSET; }
 
 // ---- Init (compaction.tla:188-202), world == 1: initial state idx goes to
 // store position idx, which is also TLC's enumeration order.
+template <typename W>
 __global__ __launch_bounds__(BLOCK) void k_init_direct(Layout L, u64 n_init, u64* __restrict__ slots, int log2,
-                                                       u64* __restrict__ states, u64* __restrict__ parents,
+                                                       W* __restrict__ states, u64* __restrict__ parents,
                                                        LevelCtr* ctr) {
   const u64 idx = (u64)blockIdx.x * BLOCK + threadIdx.x;
   if (idx >= n_init) return;
-  const u64 s = init_state(L, idx);
+  const W s = init_state<W>(L, idx);
   u64 slot;
-  const int r = fpset_put(slots, log2, s, mix64(s), &slot);
-  if (r < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+  const int r = fpset_put(slots, log2, s, mixw(s), &slot);
+  if (r < 0) atomicOr(&ctr->overflow, ovf_of(r));
   if (r == 0) atomicOr(&ctr->overflow, (unsigned)OVF_DUP_INIT);
   states[idx] = s;
   parents[idx] = NO_PARENT;
@@ -71,23 +78,25 @@ __global__ __launch_bounds__(BLOCK) void k_init_direct(Layout L, u64 n_init, u64
 }
 
 // ---- Init, world > 1: keep only the initial states this rank owns.
+template <typename W>
 __global__ __launch_bounds__(BLOCK) void k_init_part(Layout L, u64 n_init, int rank, int world, u64 owner_mask,
-                                                     u64* __restrict__ slots, int log2, u64* __restrict__ states,
+                                                     u64* __restrict__ slots, int log2, W* __restrict__ states,
                                                      u64* __restrict__ parents, u64 cap, LevelCtr* ctr) {
-  __shared__ u64 s_st[BLOCK], s_par[BLOCK];
+  __shared__ W s_st[BLOCK];
+  __shared__ u64 s_par[BLOCK];
   __shared__ unsigned s_cnt;
   __shared__ unsigned long long s_base;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   const u64 idx = (u64)blockIdx.x * BLOCK + threadIdx.x;
   bool mine = false;
-  u64 s = 0;
+  W s = 0;
   if (idx < n_init) {
-    s = init_state(L, idx);
+    s = init_state<W>(L, idx);
     if (owner_of(s, owner_mask, world) == rank) {
       u64 slot;
-      const int r = fpset_put(slots, log2, s, mix64(s), &slot);
-      if (r < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+      const int r = fpset_put(slots, log2, s, mixw(s), &slot);
+      if (r < 0) atomicOr(&ctr->overflow, ovf_of(r));
       mine = r == 1;
       if (mine) {
         const int c = check_invariants(L, s);
@@ -95,7 +104,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_part(Layout L, u64 n_init, int r
       }
     }
   }
-  stage_append<false>(mine, s, NO_PARENT, 0, s_st, s_par, nullptr, &s_cnt);
+  stage_append<false, W>(mine, s, NO_PARENT, 0, s_st, s_par, nullptr, &s_cnt);
   __syncthreads();
   if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&ctr->n_new, (unsigned long long)s_cnt) : 0;
   __syncthreads();
@@ -112,9 +121,9 @@ __global__ __launch_bounds__(BLOCK) void k_init_part(Layout L, u64 n_init, int r
 }
 
 // ---- one BFS level ----
-template <bool PRODUCER, bool TLC, bool PART>
+template <typename W, bool PRODUCER, bool TLC, bool PART>
 __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
-  __shared__ u64 s_st[STAGE_CAP];
+  __shared__ W s_st[STAGE_CAP];
   __shared__ u64 s_par[STAGE_CAP];
   __shared__ u64 s_slot[TLC ? STAGE_CAP : 1];
   __shared__ unsigned s_cnt;
@@ -127,7 +136,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
   unsigned long long ev = NO_EVENT;
 
   // emit one successor (all lanes of the wave call this)
-  auto emit = [&](bool pred, u64 t, u64 dkey) {
+  auto emit = [&](bool pred, W t, u64 dkey) {
     bool isnew = false;
     u64 slot = 0;
     if (pred) {
@@ -139,7 +148,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
           const unsigned long long pos = atomicAdd(&a.ctr->n_out[dst], 1ull);
           if (pos < a.outbox_cap) {
             u64* rec = a.outbox + 2 * ((u64)dst * a.outbox_cap + pos);
-            rec[0] = t;
+            rec[0] = (u64)t;  // PART: one-word states only (tlcg_create)
             rec[1] = a.rank_tag | dkey;
           } else {
             atomicOr(&a.ctr->overflow, (unsigned)OVF_OUTBOX);
@@ -147,8 +156,8 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
         }
       }
       if (local) {
-        const int r = fpset_put(a.slots, a.log2, t, mix64(t), &slot);
-        if (r < 0) atomicOr(&a.ctr->overflow, (unsigned)OVF_FPSET);
+        const int r = fpset_put(a.slots, a.log2, t, mixw(t), &slot);
+        if (r < 0) atomicOr(&a.ctr->overflow, ovf_of(r));
         isnew = r == 1;
         if (TLC && r >= 0) atomicMin((unsigned long long*)&a.dkey_slot[slot], (unsigned long long)dkey);
         if (!TLC && isnew) {
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
         }
       }
     }
-    stage_append<TLC>(isnew, t, a.rank_tag | dkey, slot, s_st, s_par, s_slot, &s_cnt);
+    stage_append<TLC, W>(isnew, t, a.rank_tag | dkey, slot, s_st, s_par, s_slot, &s_cnt);
   };
 
   auto flush = [&]() {
@@ -168,7 +177,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
     const u64 b = s_base;
     if (b + n <= a.cap_out) {
       for (unsigned i = threadIdx.x; i < n; i += BLOCK) {
-        a.states_out[b + i] = s_st[i];
+        reinterpret_cast<W*>(a.states_out)[b + i] = s_st[i];
         a.parents_out[b + i] = s_par[i];
         if (TLC) a.slot_out[b + i] = s_slot[i];
       }
@@ -196,7 +205,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
     for (int it = 0; it < kItems; ++it) {
       const u64 pi = c0 + (u64)it * BLOCK + threadIdx.x;
       const bool valid = pi < a.n_front;
-      const u64 s = valid ? a.frontier[pi] : 0;
+      const W s = valid ? reinterpret_cast<const W*>(a.frontier)[pi] : (W)0;
       const u64 dk0 = (a.front_gidx0 + pi) << L.ord_bits;
       int nsucc = 0;
       if (PRODUCER) {  // Producer, compaction.tla:83-87
@@ -205,20 +214,20 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
 #pragma unroll 1
         for (int j = 0; j < L.nkv; ++j) {
           if ((j & 3) == 0) reserve(6);
-          emit(can, can ? producer_succ(L, s, len, j) : 0, dk0 | (u64)j);
+          emit(can, can ? producer_succ(L, s, len, j) : (W)0, dk0 | (u64)j);
         }
         nsucc += can ? L.nkv : 0;
         reserve(2);
       }
       // the compactor disjuncts, compaction.tla:221-226
-      u64 t = 0;
+      W t = 0;
       int act = 0;
       const int r = valid ? compactor_step(L, s, &t, &act) : 0;
       if (r == 2) ev = min(ev, (unsigned long long)make_event(dk0 | (u64)ordinal_of(L, act, 0), EVK_ACTION_ERROR, act));
       nsucc += (r == 1);
       emit(r == 1, t, dk0 | (u64)ordinal_of(L, act, 0));
       // BrokerCrash, compaction.tla:227
-      u64 t2 = 0;
+      W t2 = 0;
       const bool en2 = valid && crash_step(L, s, &t2);
       nsucc += en2;
       emit(en2, t2, dk0 | (u64)ordinal_of(L, ACT_CRASH, 0));
@@ -328,7 +337,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_fast(ExpandArgs a) {
         const int q = check_invariants(L, cand[c]);
         if (q >= 0) ev = min(ev, (unsigned long long)make_event(dk[c], (q & 1) ? EVK_INV_ERROR : EVK_VIOLATION, q >> 1));
       }
-      stage_append<false>(isnew[c], cand[c], a.rank_tag | dk[c], 0, s_st, s_par, nullptr, &s_cnt);
+      stage_append<false, u64>(isnew[c], cand[c], a.rank_tag | dk[c], 0, s_st, s_par, nullptr, &s_cnt);
     }
     // flush the stage: one global atomic per block chunk
     __syncthreads();
@@ -362,12 +371,14 @@ __global__ __launch_bounds__(BLOCK) void k_gather_dkey(u64 n, const u64* __restr
 
 // ---- TLC order: write the level back in discovery order, parent = first
 // discoverer, invariants on each new state keyed by its discovery key.
-__global__ __launch_bounds__(BLOCK) void k_tlc_finish(Layout L, u64 n, const u64* __restrict__ st_sorted,
-                                                      const u64* __restrict__ dk_sorted, u64* __restrict__ states,
+template <typename W>
+__global__ __launch_bounds__(BLOCK) void k_tlc_finish(Layout L, u64 n, const W* __restrict__ st_sorted,
+                                                      const u64* __restrict__ dk_sorted, W* __restrict__ states,
                                                       u64* __restrict__ parents, u64 rank_tag, LevelCtr* ctr) {
   const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
-  const u64 s = st_sorted[i], dk = dk_sorted[i];
+  const W s = st_sorted[i];
+  const u64 dk = dk_sorted[i];
   states[i] = s;
   parents[i] = rank_tag | dk;
   const int c = check_invariants(L, s);
@@ -375,13 +386,15 @@ __global__ __launch_bounds__(BLOCK) void k_tlc_finish(Layout L, u64 n, const u64
 }
 
 // ---- FPSet growth: re-insert every stored state
-__global__ __launch_bounds__(BLOCK) void k_reinsert(const u64* __restrict__ states, u64 n, u64* __restrict__ slots,
+template <typename W>
+__global__ __launch_bounds__(BLOCK) void k_reinsert(const W* __restrict__ states, u64 n, u64* __restrict__ slots,
                                                     int log2, LevelCtr* ctr) {
   const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
-  const u64 s = states[i];
+  const W s = states[i];
   u64 slot;
-  if (fpset_put(slots, log2, s, mix64(s), &slot) < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+  const int r = fpset_put(slots, log2, s, mixw(s), &slot);
+  if (r < 0) atomicOr(&ctr->overflow, ovf_of(r));
 }
 
 // ---- world > 1: insert successors received from other ranks
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(BLOCK) void k_absorb(Layout L, const u64* __restric
     ref = recs[2 * i + 1];
     u64 slot;
     const int r = fpset_put(slots, log2, t, mix64(t), &slot);
-    if (r < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+    if (r < 0) atomicOr(&ctr->overflow, ovf_of(r));
     isnew = r == 1;
     if (isnew) {
       const int c = check_invariants(L, t);
@@ -410,7 +423,7 @@ __global__ __launch_bounds__(BLOCK) void k_absorb(Layout L, const u64* __restric
         atomicMin(&ctr->event, make_event((1ull << 51) | i, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
     }
   }
-  stage_append<false>(isnew, t, ref, 0, s_st, s_par, nullptr, &s_cnt);
+  stage_append<false, u64>(isnew, t, ref, 0, s_st, s_par, nullptr, &s_cnt);
   __syncthreads();
   if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&ctr->n_new, (unsigned long long)s_cnt) : 0;
   __syncthreads();
@@ -440,6 +453,7 @@ struct tlcg_ctx {
   tlcg_model model;
   tlcg_opts opts;
   HostModel hm;
+  int words = 1;  // u64 words per state: 1, or 2 for wide layouts (> 63 bits)
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
@@ -501,7 +515,7 @@ struct tlcg_ctx {
   int status = TLCG_RUNNING;
   u64 ev_word = NO_EVENT;
   int ev_level = -1;  // level whose expansion raised the event (0 = Init)
-  u64 ev_state = 0;
+  u128 ev_state = 0;
   u64 ev_parent_gidx = NO_PARENT;
   u64 ev_parent_ref = NO_PARENT;
   int ev_action = -1;
@@ -558,15 +572,15 @@ bool ensure_store(tlcg_ctx* c, u64 need) {
   ncap = std::max<u64>(ncap, 1u << 16);
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
-    u64 room = (u64)(fr * 0.9) / 16 + c->cap;  // both arrays; old ones freed after copy
+    u64 room = (u64)(fr * 0.9) / (8 * (c->words + 1)) + c->cap;  // both arrays; old ones freed after copy
     if (ncap > room && need <= room) ncap = room;
   }
   u64 *ns = nullptr, *np = nullptr;
-  if (!alloc_bytes(c, (void**)&ns, ncap * 8, "state store")) return false;
+  if (!alloc_bytes(c, (void**)&ns, ncap * 8 * c->words, "state store")) return false;
   if (!alloc_bytes(c, (void**)&np, ncap * 8, "parent log")) { hipFree(ns); return false; }
   const u64 keep = std::min<u64>(c->cap, store_end(c) + c->pending);
   if (keep) {
-    HIPCHK(hipMemcpyAsync(ns, c->d_states, keep * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(ns, c->d_states, keep * 8 * c->words, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(np, c->d_parents, keep * 8, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }
@@ -585,16 +599,21 @@ bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
     c->d_slots = nullptr;
     hipFree(c->d_dkey_slot);
     c->d_dkey_slot = nullptr;
-    if (!alloc_bytes(c, (void**)&c->d_slots, (8ull << log2), "FPSet")) return false;
+    if (!alloc_bytes(c, (void**)&c->d_slots, ((8ull * c->words) << log2), "FPSet")) return false;
     if (c->opts.tlc_order && !alloc_bytes(c, (void**)&c->d_dkey_slot, (8ull << log2), "FPSet discovery keys"))
       return false;
     c->log2 = log2;
   }
-  HIPCHK(hipMemsetAsync(c->d_slots, 0, 8ull << log2, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_slots, 0, (8ull * c->words) << log2, c->stream));
   if (c->d_dkey_slot) HIPCHK(hipMemsetAsync(c->d_dkey_slot, 0xFF, 8ull << log2, c->stream));
   if (n) {
     HIPCHK(hipMemsetAsync(c->d_aux, 0, sizeof(LevelCtr), c->stream));
-    k_reinsert<<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(c->d_states, n, c->d_slots, log2, c->d_aux);
+    if (c->words == 1)
+      k_reinsert<u64><<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(c->d_states, n, c->d_slots, log2,
+                                                                               c->d_aux);
+    else
+      k_reinsert<u128><<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>((const u128*)c->d_states, n,
+                                                                                c->d_slots, log2, c->d_aux);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_aux, c->d_aux, sizeof(LevelCtr), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -625,11 +644,15 @@ bool ensure_scratch(tlcg_ctx* c, u64 n) {
   if (!alloc_bytes(c, (void**)&c->d_slot_new, ncap * 8, "TLC-order scratch")) return false;
   if (!alloc_bytes(c, (void**)&c->d_dk, ncap * 8, "TLC-order scratch")) return false;
   if (!alloc_bytes(c, (void**)&c->d_dk2, ncap * 8, "TLC-order scratch")) return false;
-  if (!alloc_bytes(c, (void**)&c->d_st2, ncap * 8, "TLC-order scratch")) return false;
+  if (!alloc_bytes(c, (void**)&c->d_st2, ncap * 8 * c->words, "TLC-order scratch")) return false;
   size_t tmp = 0;
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const u64*)nullptr, (u64*)nullptr, (const u64*)nullptr,
-                                            (u64*)nullptr, (int)std::min<u64>(ncap, 0x7fffffffull), 0, 64,
-                                            c->stream));
+  const int nmax = (int)std::min<u64>(ncap, 0x7fffffffull);
+  if (c->words == 1)
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const u64*)nullptr, (u64*)nullptr, (const u64*)nullptr,
+                                              (u64*)nullptr, nmax, 0, 64, c->stream));
+  else
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const u64*)nullptr, (u64*)nullptr, (const u128*)nullptr,
+                                              (u128*)nullptr, nmax, 0, 64, c->stream));
   if (!alloc_bytes(c, &c->d_sort_tmp, tmp, "sort scratch")) return false;
   c->sort_tmp_bytes = tmp;
   c->scratch_cap = ncap;
@@ -678,10 +701,21 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   st->levels_redone = c->levels_redone;
 }
 
-bool state_at(tlcg_ctx* c, u64 g, u64* s, u64* p) {
-  HIPCHK(hipMemcpy(s, c->d_states + g, 8, hipMemcpyDeviceToHost));
+bool state_at(tlcg_ctx* c, u64 g, u128* s, u64* p) {
+  uint64_t w[2] = {0, 0};
+  HIPCHK(hipMemcpy(w, c->d_states + g * c->words, 8 * c->words, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(p, c->d_parents + g, 8, hipMemcpyDeviceToHost));
+  *s = join_words(w, c->words);
   return true;
+}
+
+// successor at a Next ordinal of a state held as u128 (either width)
+int successor_at_any(const tlcg_ctx* c, u128 s, int ord, u128* t) {
+  if (c->words == 2) return successor_at<u128>(c->hm.L, s, ord, t);
+  u64 t1 = 0;
+  const int r = successor_at<u64>(c->hm.L, (u64)s, ord, &t1);
+  *t = t1;
+  return r;
 }
 
 // Interpret the level's event word (world == 1 or a local event).
@@ -699,7 +733,7 @@ bool resolve_event(tlcg_ctx* c, u64 ev, int level) {
     default: c->status = TLCG_ACTION_ERROR; break;
   }
   if (level == 0) {  // an initial state (dkey = enumeration index)
-    c->ev_state = init_state(L, dkey);
+    c->ev_state = c->words == 2 ? init_state<u128>(L, dkey) : (u128)init_state<u64>(L, dkey);
     c->ev_parent_gidx = NO_PARENT;
     c->ev_action = TLCG_ACT_INIT;
     return true;
@@ -716,7 +750,8 @@ bool resolve_event(tlcg_ctx* c, u64 ev, int level) {
   }
   const u64 pg = dkey >> L.ord_bits;
   const int ord = (int)(dkey & ((1ull << L.ord_bits) - 1));
-  u64 ps = 0, pp = 0;
+  u128 ps = 0;
+  u64 pp = 0;
   if (!state_at(c, pg, &ps, &pp)) return false;
   c->ev_parent_gidx = pg;
   c->ev_parent_ref = ((u64)c->opts.rank << 56) | dkey;
@@ -727,8 +762,8 @@ bool resolve_event(tlcg_ctx* c, u64 ev, int level) {
     c->ev_state = ps;
     c->ev_action = index;
   } else {
-    u64 t = 0;
-    if (successor_at(L, ps, ord, &t) != 1) {
+    u128 t = 0;
+    if (successor_at_any(c, ps, ord, &t) != 1) {
       c->err = "internal: violating successor could not be re-derived";
       return false;
     }
@@ -777,7 +812,8 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
     c->err = "internal: component of the event not found";
     return false;
   }
-  u64 ps = 0, pp = 0;
+  u128 ps = 0;
+  u64 pp = 0;
   if (!state_at(c, gidx, &ps, &pp)) return false;
   c->ev_parent_gidx = gidx;
   c->ev_parent_ref = ((u64)c->opts.rank << 56) | (gidx << L.ord_bits);
@@ -788,8 +824,8 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
     c->ev_state = ps;
     c->ev_action = action;
   } else {
-    u64 t = 0;
-    if (successor_at(L, ps, ordinal_of(L, action, 0), &t) != 1) {
+    u128 t = 0;
+    if (successor_at_any(c, ps, ordinal_of(L, action, 0), &t) != 1) {
       c->err = "internal: violating successor could not be re-derived";
       return false;
     }
@@ -806,7 +842,7 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
 bool component_applicable(const tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   const int mb = L.msg_sh + L.N * L.mw;
-  return !L.producer && !c->opts.tlc_order && c->closed && L.bits - mb <= 32 && L.N <= 8 &&
+  return !L.producer && !c->opts.tlc_order && c->closed && L.bits <= 63 && L.bits - mb <= 32 && L.N <= 8 &&
          c->hm.n_init < (1ull << 36);
 }
 
@@ -948,13 +984,19 @@ bool run_init(tlcg_ctx* c) {
   for (;;) {
     if (!reset_ctr(c)) return false;
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
-    if (world == 1) {
-      k_init_direct<<<grid_for(hm.n_init, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
-          L, hm.n_init, c->d_slots, c->log2, c->d_states, c->d_parents, c->d_ctr);
+    const unsigned g = grid_for(hm.n_init, BLOCK, 0x7fffffffu);
+    if (world == 1 && c->words == 1) {
+      k_init_direct<u64><<<g, BLOCK, 0, c->stream>>>(L, hm.n_init, c->d_slots, c->log2, c->d_states, c->d_parents,
+                                                     c->d_ctr);
+    } else if (world == 1) {
+      k_init_direct<u128><<<g, BLOCK, 0, c->stream>>>(L, hm.n_init, c->d_slots, c->log2, (u128*)c->d_states,
+                                                      c->d_parents, c->d_ctr);
+    } else if (c->words == 1) {
+      k_init_part<u64><<<g, BLOCK, 0, c->stream>>>(L, hm.n_init, c->opts.rank, world, c->owner_mask, c->d_slots,
+                                                   c->log2, c->d_states, c->d_parents, c->cap, c->d_ctr);
     } else {
-      k_init_part<<<grid_for(hm.n_init, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
-          L, hm.n_init, c->opts.rank, world, c->owner_mask, c->d_slots, c->log2, c->d_states, c->d_parents,
-          c->cap, c->d_ctr);
+      k_init_part<u128><<<g, BLOCK, 0, c->stream>>>(L, hm.n_init, c->opts.rank, world, c->owner_mask, c->d_slots,
+                                                    c->log2, (u128*)c->d_states, c->d_parents, c->cap, c->d_ctr);
     }
     HIPCHK_I(hipGetLastError());
     HIPCHK_I(hipEventRecord(c->e1, c->stream));
@@ -965,6 +1007,10 @@ bool run_init(tlcg_ctx* c) {
     const unsigned ovf = c->h_ctr->overflow;
     if (ovf & OVF_DUP_INIT) {
       c->err = "internal: duplicate initial state";
+      return false;
+    }
+    if (ovf & OVF_WIDE_SPIN) {
+      c->err = "internal: wide FPSet slot never published";
       return false;
     }
     if (!ovf) break;
@@ -985,21 +1031,22 @@ bool run_init(tlcg_ctx* c) {
 }
 
 template <bool P, bool T, bool X>
-void launch_expand_t(const ExpandArgs& a, unsigned grid, hipStream_t s) {
-  k_expand<P, T, X><<<grid, BLOCK, 0, s>>>(a);
+void launch_expand_t(const ExpandArgs& a, unsigned grid, hipStream_t s, int words) {
+  if (words == 1) k_expand<u64, P, T, X><<<grid, BLOCK, 0, s>>>(a);
+  else if constexpr (!X) k_expand<u128, P, T, false><<<grid, BLOCK, 0, s>>>(a);  // wide: closed partitions only
 }
 
 bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
   const Layout& L = c->hm.L;
   ExpandArgs a;
   a.L = L;
-  a.frontier = c->d_states + front0;
+  a.frontier = c->d_states + front0 * c->words;
   a.n_front = n_front;
   a.front_gidx0 = front0;
   a.slots = c->d_slots;
   a.log2 = c->log2;
   const u64 d = distinct_of(c);
-  a.states_out = c->d_states + d;
+  a.states_out = c->d_states + d * c->words;
   a.parents_out = c->d_parents + d;
   a.cap_out = c->cap - d;
   a.slot_out = c->d_slot_new;
@@ -1012,7 +1059,7 @@ bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
   a.outbox = c->d_outbox;
   a.outbox_cap = c->outbox_cap;
   const bool prod = L.producer != 0, tlc = c->opts.tlc_order != 0;
-  if (!prod && !tlc && !part && c->fast_items > 0) {
+  if (!prod && !tlc && !part && c->fast_items > 0 && c->words == 1) {
     const int it = c->fast_items;
     const unsigned g = grid_for(n_front, (u64)BLOCK * it, c->grid_cap);
     if (c->probe_mode == 0) {
@@ -1029,14 +1076,15 @@ bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
   }
   const u64 per_block = (u64)BLOCK * (prod ? 1 : ITEMS);
   const unsigned grid = grid_for(n_front, per_block, c->grid_cap);
+  const int w = c->words;
   if (prod) {
-    if (tlc) launch_expand_t<true, true, false>(a, grid, c->stream);
-    else if (part) launch_expand_t<true, false, true>(a, grid, c->stream);
-    else launch_expand_t<true, false, false>(a, grid, c->stream);
+    if (tlc) launch_expand_t<true, true, false>(a, grid, c->stream, w);
+    else if (part) launch_expand_t<true, false, true>(a, grid, c->stream, w);
+    else launch_expand_t<true, false, false>(a, grid, c->stream, w);
   } else {
-    if (tlc) launch_expand_t<false, true, false>(a, grid, c->stream);
-    else if (part) launch_expand_t<false, false, true>(a, grid, c->stream);
-    else launch_expand_t<false, false, false>(a, grid, c->stream);
+    if (tlc) launch_expand_t<false, true, false>(a, grid, c->stream, w);
+    else if (part) launch_expand_t<false, false, true>(a, grid, c->stream, w);
+    else launch_expand_t<false, false, false>(a, grid, c->stream, w);
   }
   HIPCHK_I(hipGetLastError());
   return true;
@@ -1053,10 +1101,20 @@ bool tlc_order_level(tlcg_ctx* c, u64 n_new) {
   HIPCHK_I(hipGetLastError());
   const int end_bit = std::min(64, bits_for(((d + n_new) << L.ord_bits) | ((1ull << L.ord_bits) - 1)));
   size_t tmp = c->sort_tmp_bytes;
-  HIPCHK_I(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, c->d_states + d, c->d_st2,
-                                            (int)n_new, 0, end_bit, c->stream));
-  k_tlc_finish<<<grid_for(n_new, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
-      L, n_new, c->d_st2, c->d_dk2, c->d_states + d, c->d_parents + d, (u64)c->opts.rank << 56, c->d_ctr);
+  const unsigned g = grid_for(n_new, BLOCK, 0x7fffffffu);
+  const u64 tag = (u64)c->opts.rank << 56;
+  if (c->words == 1) {
+    HIPCHK_I(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, c->d_states + d, c->d_st2,
+                                                (int)n_new, 0, end_bit, c->stream));
+    k_tlc_finish<u64><<<g, BLOCK, 0, c->stream>>>(L, n_new, c->d_st2, c->d_dk2, c->d_states + d, c->d_parents + d,
+                                                  tag, c->d_ctr);
+  } else {
+    u128* st = (u128*)c->d_states + d;
+    HIPCHK_I(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, (const u128*)st,
+                                                (u128*)c->d_st2, (int)n_new, 0, end_bit, c->stream));
+    k_tlc_finish<u128><<<g, BLOCK, 0, c->stream>>>(L, n_new, (const u128*)c->d_st2, c->d_dk2, st, c->d_parents + d,
+                                                   tag, c->d_ctr);
+  }
   HIPCHK_I(hipGetLastError());
   return true;
 }
@@ -1110,6 +1168,10 @@ bool step_level(tlcg_ctx* c) {
     c->kernel_ms += ms_all;
     const unsigned ovf = c->h_ctr->overflow;
     if (!ovf) break;
+    if (ovf & OVF_WIDE_SPIN) {
+      c->err = "internal: wide FPSet slot never published";
+      return false;
+    }
     // grow and redo the level from the committed levels
     ++c->levels_redone;
     if (ovf & OVF_STORE) {
@@ -1152,11 +1214,18 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
     *out = c;
     return -3;
   }
+  c->words = state_words(c->hm.L);
   // partition key: `messages` alone when it is immutable (no Producer), so a
   // state's whole successor graph stays on its owner rank; else the state.
   const int part = c->opts.partition ? c->opts.partition : (c->hm.L.producer ? 2 : 1);
   c->owner_mask = part == 1 ? c->hm.L.msgs_mask : ~0ull;
   c->closed = c->opts.world == 1 || (part == 1 && !c->hm.L.producer);
+  if (c->words == 2 && c->opts.world > 1 && (!c->closed || c->hm.L.msgs_mask_hi)) {
+    c->err = "wide (> 63-bit) states are partitioned only by an immutable `messages` held in the low word "
+             "(no Producer, partition 0/1)";
+    *out = c;
+    return -2;
+  }
   if (c->opts.engine == TLCG_ENGINE_COMPONENT && !component_applicable(c)) {
     c->err = "the component engine needs an immutable `messages` (no Producer), no TLC-order mode and a closed partition";
     *out = c;
@@ -1292,25 +1361,42 @@ int tlcg_level_sizes(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
   return 0;
 }
 
-int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref) {
+int tlcg_state_at_words(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref) {
   if (!c || gidx >= store_end(c)) return -1;
-  u64 s = 0, p = 0;
+  u128 s = 0;
+  u64 p = 0;
   if (!state_at(c, gidx, &s, &p)) return -10;
-  if (state) *state = s;
+  if (state) split_words(s, state, c->words);
   if (parent_ref) *parent_ref = p;
   return 0;
 }
 
-int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
+int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref) {
+  if (c && c->words != 1) {
+    c->err = "a wide (> 63-bit) state: use tlcg_state_at_words";
+    return -2;
+  }
+  return tlcg_state_at_words(c, gidx, state, parent_ref);
+}
+
+int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
   if (!c || first + n > store_end(c)) return -1;
-  if (n && hipMemcpy(out, c->d_states + first, n * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+  if (n && hipMemcpy(out, c->d_states + first * c->words, n * 8 * c->words, hipMemcpyDeviceToHost) != hipSuccess) {
     c->err = "copy failed";
     return -10;
   }
   return 0;
 }
 
-int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len) {
+int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
+  if (c && c->words != 1) {
+    c->err = "wide (> 63-bit) states: use tlcg_copy_states_words";
+    return -2;
+  }
+  return tlcg_copy_states_words(c, first, n, out);
+}
+
+int tlcg_trace_words(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len) {
   if (!c) return -1;
   if (c->ev_word == NO_EVENT) {
     c->err = "no violation to trace";
@@ -1318,7 +1404,7 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
   }
   const Layout& L = c->hm.L;
   const u64 ordmask = (1ull << L.ord_bits) - 1;
-  std::vector<u64> st;
+  std::vector<u128> st;
   std::vector<int> act;
   if (c->ev_level == 0) {
     st.push_back(c->ev_state);
@@ -1330,7 +1416,8 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
     }
     u64 g = c->ev_parent_gidx;
     for (;;) {
-      u64 s, p;
+      u128 s;
+      u64 p;
       if (!state_at(c, g, &s, &p)) return -10;
       st.push_back(s);
       if (p == NO_PARENT) {
@@ -1353,11 +1440,19 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
   }
   const int n = (int)st.size();
   for (int i = 0; i < n && i < cap; ++i) {
-    if (states) states[i] = st[(size_t)i];
+    if (states) split_words(st[(size_t)i], states + (size_t)i * c->words, c->words);
     if (actions) actions[i] = act[(size_t)i];
   }
   if (len) *len = n;
   return 0;
+}
+
+int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len) {
+  if (c && c->words != 1) {
+    c->err = "a wide (> 63-bit) state: use tlcg_trace_words";
+    return -2;
+  }
+  return tlcg_trace_words(c, states, actions, cap, len);
 }
 
 int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t cap) {
@@ -1374,7 +1469,7 @@ int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t 
 }
 
 int tlcg_owner(tlcg_ctx* c, uint64_t state) {
-  if (!c) return -1;
+  if (!c) return -1;  // wide states: pass the low word (the partition key lies there)
   return (int)(((mix64(state & c->owner_mask) >> 32) * (u64)c->opts.world) >> 32);
 }
 

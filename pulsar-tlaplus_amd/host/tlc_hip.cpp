@@ -219,16 +219,17 @@ int main(int argc, char** argv) {
         break;
     }
     if (o.trace) {
-      std::vector<uint64_t> states(1 << 16);
+      const int words = tlcg_state_words(&model);  // 1, or 2 for a > 63-bit layout
+      std::vector<uint64_t> states((size_t)words << 16);
       std::vector<int32_t> acts(1 << 16);
       int32_t n = 0;
-      if (tlcg_trace(tctx, states.data(), acts.data(), (int32_t)states.size(), &n) == 0) {
+      if (tlcg_trace_words(tctx, states.data(), acts.data(), (int32_t)acts.size(), &n) == 0) {
         std::printf("Error: The behavior up to this point is:\n");
         std::vector<char> buf(1 << 16);
         for (int i = 0; i < n; ++i) {
           if (acts[(size_t)i] < 0) std::printf("State %d: <Initial predicate>\n", i + 1);
           else std::printf("State %d: <%s>\n", i + 1, action_location(mod, acts[(size_t)i]).c_str());
-          tlcg_decode(&model, states[(size_t)i], buf.data(), (int32_t)buf.size());
+          tlcg_decode_words(&model, &states[(size_t)i * words], buf.data(), (int32_t)buf.size());
           std::printf("%s\n\n", buf.data());
         }
       } else {

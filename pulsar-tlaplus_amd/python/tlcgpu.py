@@ -96,6 +96,14 @@ def load_library(path: str = LIB_PATH):
         "tlcg_absorb": (C.c_int, [P, U64, S]),
         "tlcg_end_level": (C.c_int, [P, S]),
         "tlcg_outbox_read": (C.c_int, [P, I32, P, U64]),
+        "tlcg_state_words": (C.c_int, [M]),
+        "tlcg_decode_words": (C.c_int, [M, C.POINTER(U64), C.c_char_p, I32]),
+        "tlcg_host_init_state_words": (C.c_int, [M, U64, C.POINTER(U64)]),
+        "tlcg_host_successors_words": (C.c_int, [M, C.POINTER(U64), C.POINTER(U64), C.POINTER(I32), I32]),
+        "tlcg_host_check_invariants_words": (C.c_int, [M, C.POINTER(U64)]),
+        "tlcg_trace_words": (C.c_int, [P, C.POINTER(U64), C.POINTER(I32), I32, C.POINTER(I32)]),
+        "tlcg_state_at_words": (C.c_int, [P, U64, C.POINTER(U64), C.POINTER(U64)]),
+        "tlcg_copy_states_words": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
         "tlcg_absorb_records": (C.c_int, [P, P, U64, S]),
         "tlcg_stream": (P, [P]),
         "tlcg_jit_selftest": (C.c_int, [M, C.c_char_p, I32, C.c_char_p, I32][:1] + [C.c_char_p, C.c_char_p, I32]),
@@ -178,11 +186,26 @@ def init_count(model: Model) -> int:
     return load_library().tlcg_init_count(C.byref(m))
 
 
+def state_words(model: Model) -> int:
+    """uint64 words per packed state: 1 (<= 63 bits) or 2 (wide, <= 126 bits)."""
+    m = model.to_c()
+    return load_library().tlcg_state_words(C.byref(m))
+
+
+def _to_words(state: int, w: int):
+    return (C.c_uint64 * w)(*[(state >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(w)])
+
+
+def _from_words(buf, i: int, w: int) -> int:
+    return sum(int(buf[i * w + k]) << (64 * k) for k in range(w))
+
+
 def decode(model: Model, state: int) -> str:
+    """TLC value syntax of a packed state (a Python int of either width)."""
     lib = load_library()
     m = model.to_c()
     buf = C.create_string_buffer(1 << 16)
-    n = lib.tlcg_decode(C.byref(m), C.c_uint64(state), buf, len(buf))
+    n = lib.tlcg_decode_words(C.byref(m), _to_words(state, state_words(model)), buf, len(buf))
     if n < 0:
         raise ValueError("bad model")
     return buf.value.decode()
@@ -190,19 +213,24 @@ def decode(model: Model, state: int) -> str:
 
 def host_init_state(model: Model, idx: int) -> int:
     m = model.to_c()
-    return load_library().tlcg_host_init_state(C.byref(m), idx)
+    w = state_words(model)
+    out = (C.c_uint64 * 2)()
+    if load_library().tlcg_host_init_state_words(C.byref(m), idx, out) != 0:
+        raise ValueError("bad model")
+    return _from_words(out, 0, w)
 
 
 def host_successors(model: Model, state: int) -> List[Tuple[str, int]]:
     lib = load_library()
     m = model.to_c()
+    w = state_words(model)
     cap = 8192
-    out = (C.c_uint64 * cap)()
+    out = (C.c_uint64 * (cap * w))()
     acts = (C.c_int32 * cap)()
-    n = lib.tlcg_host_successors(C.byref(m), C.c_uint64(state), out, acts, cap)
+    n = lib.tlcg_host_successors_words(C.byref(m), _to_words(state, w), out, acts, cap)
     if n < 0:
         raise RuntimeError("evaluation error")
-    return [(ACTIONS[acts[i]], out[i]) for i in range(n)]
+    return [(ACTIONS[acts[i]], _from_words(out, i, w)) for i in range(n)]
 
 
 def host_component_selfcheck(model: Model, first: int, n: int) -> int:
@@ -214,7 +242,7 @@ def host_component_selfcheck(model: Model, first: int, n: int) -> int:
 
 def host_check_invariants(model: Model, state: int) -> int:
     m = model.to_c()
-    return load_library().tlcg_host_check_invariants(C.byref(m), C.c_uint64(state))
+    return load_library().tlcg_host_check_invariants_words(C.byref(m), _to_words(state, state_words(model)))
 
 
 @dataclass
@@ -256,6 +284,7 @@ class Checker:
             self.close()
             raise RuntimeError(f"tlcg_create: {msg} ({rc})")
         self.stats = tlcg_stats()
+        self.words = state_words(model)
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -292,22 +321,23 @@ class Checker:
         return [buf[i] for i in range(min(n.value, 65536))]
 
     def trace(self) -> List[Tuple[str, int]]:
-        cap = 1 << 16
-        st = (C.c_uint64 * cap)()
+        cap, w = 1 << 16, self.words
+        st = (C.c_uint64 * (cap * w))()
         ac = (C.c_int32 * cap)()
         n = C.c_int32()
-        self._chk(self.lib.tlcg_trace(self.ctx, st, ac, cap, C.byref(n)), "tlcg_trace")
-        return [("Init" if ac[i] < 0 else ACTIONS[ac[i]], st[i]) for i in range(n.value)]
+        self._chk(self.lib.tlcg_trace_words(self.ctx, st, ac, cap, C.byref(n)), "tlcg_trace_words")
+        return [("Init" if ac[i] < 0 else ACTIONS[ac[i]], _from_words(st, i, w)) for i in range(n.value)]
 
     def copy_states(self, first: int, n: int) -> List[int]:
-        buf = (C.c_uint64 * max(n, 1))()
-        self._chk(self.lib.tlcg_copy_states(self.ctx, first, n, buf), "tlcg_copy_states")
-        return list(buf[:n])
+        w = self.words
+        buf = (C.c_uint64 * (max(n, 1) * w))()
+        self._chk(self.lib.tlcg_copy_states_words(self.ctx, first, n, buf), "tlcg_copy_states_words")
+        return [_from_words(buf, i, w) for i in range(n)]
 
     def state_at(self, gidx: int) -> Tuple[int, int]:
-        s, p = C.c_uint64(), C.c_uint64()
-        self._chk(self.lib.tlcg_state_at(self.ctx, gidx, C.byref(s), C.byref(p)), "tlcg_state_at")
-        return s.value, p.value
+        s, p = (C.c_uint64 * 2)(), C.c_uint64()
+        self._chk(self.lib.tlcg_state_at_words(self.ctx, gidx, s, C.byref(p)), "tlcg_state_at_words")
+        return _from_words(s, 0, self.words), p.value
 
     def result(self, with_trace: bool = True) -> Result:
         s = self.stats

@@ -47,6 +47,20 @@ CASES = {
     "X_C5_K2": dict(N=2, C=5, K=2, keys=[1], values=[1]),
     "X_empty_spaces": dict(N=3, C=3, K=1, keys=[], values=[]),
 }
+# wide layouts (> 63 bits: two-word states, SURVEY 8(d) G9-deep family)
+CASES.update({
+    "W_C12_k1": dict(C=12, keys=[1], values=[1]),
+    "W_C12": dict(C=12),
+    "W_C12_noretain": dict(C=12, retain=False),
+    "W_C12_leak": dict(C=12, keys=[1], values=[1], invariants=["TypeSafe", "CompactedLedgerLeak"]),
+    "W_C12_dup": dict(C=12, keys=[1], values=[1], invariants=["DuplicateNullKeyMessage"]),
+    "W_P_C12": dict(C=12, keys=[1], values=[1], producer=True, retain=False),
+    "W_N4_C6": dict(N=4, C=6, keys=[1, 2, 3], values=[1]),
+    "W_N4_C6_K2_consumer": dict(N=4, C=6, K=2, keys=[1, 2, 3], values=[1], consumer=True, ctl=0),
+})
+# one M of G9-deep (KeySpace = ValueSpace = {1..10}, CompactionTimesLimit = 12)
+CASES["G9deep_first_M"] = dict(C=12, keys=list(range(1, 11)), values=list(range(1, 11)), init_range=[0, 1])
+CASES["G9deep_some_M"] = dict(C=12, keys=list(range(1, 11)), values=list(range(1, 11)), init_range=[777000, 777050])
 # R(C, K): one initial state (KeySpace = ValueSpace = {}), N = 1
 for C in range(1, 7):
     for K in range(0, 4):

@@ -67,7 +67,7 @@ def test_struct_layout_matches_c(tmp_path):
     (dict(key_space=[-1]), "KeySpace \\in SUBSET Nat"),
     (dict(msg_sent_limit=-1), "MessageSentLimit \\in Nat"),
     (dict(max_crash_times=-2), "MaxCrashTimes \\in Nat"),
-    (dict(compaction_times_limit=12, key_space=range(1, 11), value_space=range(1, 11)), "63 bits"),
+    (dict(compaction_times_limit=30, key_space=range(1, 11), value_space=range(1, 11)), "126 bits"),
 ])
 def test_check_model_rejects(kw, msg):
     err = tlcgpu.check_model(tlcgpu.Model(**kw))
@@ -95,3 +95,19 @@ def test_jit_specialization_compiles(keys):
     err = C.create_string_buffer(4096)
     n = tlcgpu.load_library().tlcg_jit_selftest(C.byref(m), b"gfx950", err, 4096)
     assert n > 0, err.value.decode()[:2000]
+
+
+def test_wide_layouts_take_two_words():
+    """> 63-bit layouts (CompactionTimesLimit = 12) are
+    accepted as two-word states; the one-word entry points refuse them."""
+    deep = tlcgpu.Model(compaction_times_limit=12, key_space=range(1, 11), value_space=range(1, 11))
+    assert tlcgpu.check_model(deep) is None
+    assert tlcgpu.state_bits(deep) > 63 and tlcgpu.state_words(deep) == 2
+    assert tlcgpu.state_words(tlcgpu.Model()) == 1
+    m = deep.to_c()
+    lib = tlcgpu.load_library()
+    assert lib.tlcg_decode(C.byref(m), 0, C.create_string_buffer(64), 64) < 0
+    s0 = tlcgpu.host_init_state(deep, 5)
+    assert "compactedLedgers = <<Nil, Nil, Nil, Nil, Nil, Nil, Nil, Nil, Nil, Nil, Nil, Nil>>" in tlcgpu.decode(deep, s0)
+    succ = tlcgpu.host_successors(deep, s0)
+    assert [a for a, _ in succ] == ["CompactorPhaseOne", "BrokerCrash"]

@@ -54,8 +54,18 @@ def test_golden_case(case, mode):
         # components are isomorphic (SURVEY App.A.1): all fit on chip iff one does
         g = GOLDEN[case]["result"]
         per_component = g["distinct"] // tlcgpu.init_count(m)
-        fits = per_component <= 255 and g["depth"] <= 47
+        fits = per_component <= 255 and g["depth"] <= 47 and component_key_fits(c)
         assert r.engine == ("component" if fits else "global"), (r.engine, per_component)
+
+
+def component_key_fits(c):
+    """the component engine's admission rule: a one-word state whose part above
+    `messages` (the local key) fits 32 bits (tlcgpu.hip component_applicable)"""
+    m = model_of(c)
+    nk, nv = len(set(c["keys"]) | {0}), len(set(c["values"]) | {0})
+    led_sh = c["N"].bit_length() + c["N"] * ((nk - 1).bit_length() + (nv - 1).bit_length())
+    bits = tlcgpu.state_bits(m)
+    return bits <= 63 and bits - led_sh <= 32 and c["N"] <= 8
 
 
 def want_ok(case):
@@ -200,3 +210,16 @@ def test_component_cascade(case, monkeypatch):
     m = model_of(GOLDEN[case]["constants"])
     r = tlcgpu.run(m)
     check_against_golden(case, r, False)
+
+
+def test_g9deep_scaled_counts():
+    """KeySpace = ValueSpace = 1..10, CompactionTimesLimit
+    = 12 -> a 93-bit state (two words, the wide FPSet): 11^6 x 557 =
+    986,759,477 distinct, 1,119,626,552 generated, depth 74."""
+    m = tlcgpu.Model(compaction_times_limit=12, **M8)
+    assert tlcgpu.state_words(m) == 2
+    r = tlcgpu.run(m, log2_fpset_slots=31, state_capacity=1_000_000_000)
+    per_m_law("G9deep_first_M", 11 ** 6, r)
+    assert (r.distinct, r.generated, r.depth) == (986_759_477, 1_119_626_552, 74)
+    assert r.engine == "global"
+
