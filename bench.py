@@ -25,6 +25,8 @@ CONFIGS = {
     "g9": dict(keys=15, distinct=1_040_187_392, generated=1_392_508_928, depth=20),
     "m8": dict(keys=10, distinct=109_836_782, generated=147_039_563, depth=20),
     "s": dict(keys=2, distinct=45_198, generated=60_507, depth=20),
+    # CompactionTimesLimit = 12, a 93-bit (two-word) state
+    "g9deep": dict(keys=10, C=12, distinct=986_759_477, generated=1_119_626_552, depth=74),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic bytes per distinct state of the fused expand kernel:
@@ -60,12 +62,17 @@ def load_microbench(rel):
 def model_for(cfg):
     import tlcgpu
     k = CONFIGS[cfg]["keys"]
-    return tlcgpu.Model(key_space=range(1, k + 1), value_space=range(1, k + 1))
+    return tlcgpu.Model(key_space=range(1, k + 1), value_space=range(1, k + 1),
+                        compaction_times_limit=CONFIGS[cfg].get("C", 3))
 
 
-def algorithmic_bytes(distinct, generated, n_init, selfloops):
+def algorithmic_bytes(distinct, generated, n_init, selfloops, words=1):
+    """read each parent, write each new state and its parent entry, one FPSet
+    slot probe per non-stuttering successor (a state and a slot are `words`
+    8-byte words; the parent entry is one)"""
     probes = generated - n_init - selfloops  # successors inserted into the FPSet
-    return BYTES_PER_STATE_WORD * (distinct + 2 * (distinct - n_init) + probes)
+    w = BYTES_PER_STATE_WORD
+    return w * words * distinct + (w * words + w) * (distinct - n_init) + w * words * probes
 
 
 def selfloops_per_m(model):
@@ -93,7 +100,8 @@ def cpu_baseline(cfg, seconds_target=12.0):
     n_m = 4096
     while True:
         t = time.time()
-        out = subprocess.run([oracle, "-keys", keys, "-values", keys, "-init-lo", "0", "-init-hi", str(n_m),
+        out = subprocess.run([oracle, "-keys", keys, "-values", keys, "-C", str(CONFIGS[cfg].get("C", 3)),
+                              "-init-lo", "0", "-init-hi", str(n_m),
                               "-notrace"], check=True, capture_output=True, text=True).stdout
         wall = time.time() - t
         r = json.loads(out)
@@ -138,6 +146,7 @@ def main():
 
     cfg = CONFIGS[args.config]
     model = model_for(args.config)
+    words = tlcgpu.state_words(model)
     import dist as tdist
 
     def time_engine(engine):
@@ -231,12 +240,14 @@ def main():
     selfloops = n_init * selfloops_per_m(model)
 
     def roofline_global(r):
-        bytes_step = algorithmic_bytes(distinct, generated, n_init, selfloops) / world  # per rank
+        abytes = algorithmic_bytes(distinct, generated, n_init, selfloops, words)
+        bytes_step = abytes / world  # per rank
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel="k_expand_fast",
+                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                  kernel="k_expand_fast" if words == 1 else "k_expand<u128> (wide FPSet)",
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=round(algorithmic_bytes(distinct, generated, n_init, selfloops) / distinct, 2))
+                  bytes_per_distinct=round(abytes / distinct, 2))
         pmc = load_profile(PMC_PROFILE)
         avg_launch_s = r["expand_ms"] / r["launches"] * 1e-3
         if pmc and args.config == "g9" and world == 1:
@@ -244,7 +255,7 @@ def main():
             rf["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_launch"])
             rf["traffic_source"] = PMC_PROFILE
         micro = load_microbench(MICRO_PROFILE)
-        if micro:
+        if micro and words == 1:
             probes = (generated - n_init - selfloops) / world
             inserts = (distinct - n_init) / world
             bound_ms = (probes / micro["load_nt"] + inserts / micro["cas_new"]) * 1e3
@@ -294,8 +305,9 @@ def main():
         "dtype": "u64",
         "data": "synthetic: the model's own state space (no external data)",
         "config": {"workload": f"compaction.tla BFS, {args.config.upper()} cfg: KeySpace = ValueSpace = "
-                               f"{{1..{cfg['keys']}}}, MessageSentLimit 3, CompactionTimesLimit 3, MaxCrashTimes 1, "
-                               f"RetainNullKey, no producer/consumer",
+                               f"{{1..{cfg['keys']}}}, MessageSentLimit 3, CompactionTimesLimit {cfg.get('C', 3)}, "
+                               f"MaxCrashTimes 1, RetainNullKey, no producer/consumer",
+                   "state_bits": tlcgpu.state_bits(model),
                    "distinct": distinct, "generated": generated, "depth": cfg["depth"],
                    "parallelism": f"partition{world}", "engine": main_s["engine"],
                    "gpu_kernel_ms_per_step": main_s["gpu_kernel_ms_per_step"]},
