@@ -211,6 +211,15 @@ int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st);
 int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n);
 int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats* st);
 
+/* TLC -checkpoint: write the run's committed levels (state store + parent
+ * log, level sizes, counters) to `path` between levels of a global-engine
+ * run (the component engine finishes inside tlcg_init). */
+int tlcg_checkpoint(tlcg_ctx* c, const char* path);
+/* TLC -recover: resume from a checkpoint taken with the same constants and
+ * options; the FPSet is rebuilt from the stored states.  Then call
+ * tlcg_step_level (or the partitioned level calls) as after tlcg_init. */
+int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st);
+
 /* Diagnostic: compile the kernels specialized for these constants (hipRTC)
  * for `arch` without a device; returns the code-object size or <0 (err). */
 int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t cap);

@@ -1455,6 +1455,187 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
   return tlcg_trace_words(c, states, actions, cap, len);
 }
 
+}  // extern "C"
+
+// ---- checkpoint / recover (TLC -checkpoint / -recover) ----
+//
+// File: CkptHeader, the tlcg_model, level_base[n_levels], then the committed
+// states (d x words uint64) and the parent log (d uint64).  The FPSet is not
+// saved: it is a function of the stored states and is rebuilt from them.
+namespace {
+
+struct CkptHeader {
+  char magic[8];
+  int32_t abi, words, rank, world, partition, tlc_order, status, pad;
+  uint64_t n_levels, generated, levels_redone, distinct;
+  double kernel_ms, expand_ms;
+};
+const char kCkptMagic[8] = {'T', 'L', 'C', 'G', 'C', 'K', 'P', '1'};
+
+bool same_constants(const tlcg_model& a, const tlcg_model& b) {
+  if (a.msg_sent_limit != b.msg_sent_limit || a.compaction_times_limit != b.compaction_times_limit ||
+      a.consume_times_limit != b.consume_times_limit || a.max_crash_times != b.max_crash_times ||
+      a.model_consumer != b.model_consumer || a.model_producer != b.model_producer ||
+      a.retain_null_key != b.retain_null_key || a.check_deadlock != b.check_deadlock || a.n_keys != b.n_keys ||
+      a.n_values != b.n_values || a.n_invariants != b.n_invariants)
+    return false;
+  for (int i = 0; i < a.n_keys; ++i)
+    if (a.keys[i] != b.keys[i]) return false;
+  for (int i = 0; i < a.n_values; ++i)
+    if (a.values[i] != b.values[i]) return false;
+  for (int i = 0; i < a.n_invariants; ++i)
+    if (a.invariants[i] != b.invariants[i]) return false;
+  return true;
+}
+
+// device <-> file through one pinned staging buffer
+constexpr size_t kStage = 64u << 20;
+
+bool dev_to_file(tlcg_ctx* c, FILE* f, const void* dev, size_t bytes, void* stage) {
+  for (size_t off = 0; off < bytes; off += kStage) {
+    const size_t n = std::min(kStage, bytes - off);
+    HIPCHK(hipMemcpyAsync(stage, (const char*)dev + off, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (std::fwrite(stage, 1, n, f) != n) {
+      c->err = "checkpoint write failed";
+      return false;
+    }
+  }
+  return true;
+}
+
+bool file_to_dev(tlcg_ctx* c, FILE* f, void* dev, size_t bytes, void* stage) {
+  for (size_t off = 0; off < bytes; off += kStage) {
+    const size_t n = std::min(kStage, bytes - off);
+    if (std::fread(stage, 1, n, f) != n) {
+      c->err = "checkpoint file is truncated";
+      return false;
+    }
+    HIPCHK(hipMemcpyAsync((char*)dev + off, stage, n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
+  if (!c || !path) return -1;
+  if (!c->inited) {
+    c->err = "nothing to checkpoint: call tlcg_init first";
+    return -2;
+  }
+  if (c->engine != TLCG_ENGINE_GLOBAL) {
+    c->err = "the component engine completes the whole check inside tlcg_init: nothing to checkpoint";
+    return -2;
+  }
+  if (c->pending || (c->status != TLCG_RUNNING && c->status != TLCG_DONE)) {
+    c->err = "a checkpoint is taken between levels of a run that has not stopped on an error";
+    return -2;
+  }
+  const u64 d = distinct_of(c);
+  CkptHeader h;
+  std::memset(&h, 0, sizeof h);
+  std::memcpy(h.magic, kCkptMagic, 8);
+  h.abi = TLCG_ABI_VERSION;
+  h.words = c->words;
+  h.rank = c->opts.rank;
+  h.world = c->opts.world;
+  h.partition = c->opts.partition;
+  h.tlc_order = c->opts.tlc_order;
+  h.status = c->status;
+  h.n_levels = c->level_base.size();
+  h.generated = c->generated;
+  h.levels_redone = c->levels_redone;
+  h.distinct = d;
+  h.kernel_ms = c->kernel_ms;
+  h.expand_ms = c->expand_ms;
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) {
+    c->err = std::string("cannot write ") + tmp;
+    return -3;
+  }
+  c->err.clear();
+  void* stage = nullptr;
+  bool ok = hipHostMalloc(&stage, kStage) == hipSuccess;
+  ok = ok && std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(&c->model, sizeof c->model, 1, f) == 1 &&
+       std::fwrite(c->level_base.data(), 8, c->level_base.size(), f) == c->level_base.size();
+  ok = ok && dev_to_file(c, f, c->d_states, d * 8 * c->words, stage) &&
+       dev_to_file(c, f, c->d_parents, d * 8, stage);
+  if (stage) hipHostFree(stage);
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok || std::rename(tmp.c_str(), path) != 0) {
+    if (c->err.empty()) c->err = std::string("checkpoint to ") + path + " failed";
+    std::remove(tmp.c_str());
+    return -3;
+  }
+  return 0;
+}
+
+int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
+  if (!c || !path) return -1;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) {
+    c->err = std::string("cannot read checkpoint ") + path;
+    return -3;
+  }
+  CkptHeader h;
+  tlcg_model m;
+  if (std::fread(&h, sizeof h, 1, f) != 1 || std::memcmp(h.magic, kCkptMagic, 8) != 0 ||
+      std::fread(&m, sizeof m, 1, f) != 1) {
+    std::fclose(f);
+    c->err = std::string(path) + " is not a tlcgpu checkpoint";
+    return -3;
+  }
+  if (h.abi != TLCG_ABI_VERSION || !same_constants(m, c->model) || h.words != c->words || h.rank != c->opts.rank ||
+      h.world != c->opts.world || h.tlc_order != c->opts.tlc_order ||
+      (h.world > 1 && h.partition != c->opts.partition) || h.n_levels < 1) {
+    std::fclose(f);
+    c->err = "the checkpoint was taken for other constants or options";
+    return -4;
+  }
+  std::vector<u64> lb(h.n_levels);
+  if (std::fread(lb.data(), 8, lb.size(), f) != lb.size() || lb.back() != h.distinct) {
+    std::fclose(f);
+    c->err = "checkpoint file is truncated";
+    return -3;
+  }
+  // the run restarts on the global engine with exactly the committed levels
+  c->engine = TLCG_ENGINE_GLOBAL;
+  c->passes.clear();
+  c->level_base.clear();
+  c->pending = 0;
+  const u64 d = h.distinct;
+  void* stage = nullptr;
+  bool ok = hipHostMalloc(&stage, kStage) == hipSuccess && ensure_store(c, d + (d >> 3) + (1u << 16));
+  ok = ok && file_to_dev(c, f, c->d_states, d * 8 * c->words, stage) &&
+       file_to_dev(c, f, c->d_parents, d * 8, stage);
+  if (stage) hipHostFree(stage);
+  std::fclose(f);
+  if (!ok) return -10;
+  c->level_base = lb;
+  c->generated = h.generated;
+  c->levels_redone = h.levels_redone;
+  c->kernel_ms = h.kernel_ms;
+  c->expand_ms = h.expand_ms;
+  c->status = h.status == TLCG_DONE ? TLCG_DONE : TLCG_RUNNING;
+  c->ev_word = NO_EVENT;
+  c->ev_level = -1;
+  c->ev_parent_gidx = NO_PARENT;
+  c->ev_parent_ref = NO_PARENT;
+  c->ev_action = -1;
+  // the FPSet is a function of the stored states: rebuild it from them
+  int l = c->opts.log2_fpset_slots > 0 ? c->opts.log2_fpset_slots : std::max(c->log2, 16);
+  while (c->opts.log2_fpset_slots <= 0 && (1ull << l) < 2 * d && l < 40) ++l;
+  if (!rebuild_fpset(c, l, d)) return -10;
+  c->inited = true;
+  fill_stats(c, st);
+  return 0;
+}
+
 int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t cap) {
   HostModel hm;
   std::string e;

@@ -5,8 +5,10 @@
 // generated, distinct states, depth, verdict and (on an error) the trace.
 #include <sys/stat.h>
 
+#include <cerrno>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <ctime>
@@ -68,14 +70,36 @@ std::string prob_str(double p) {  // Java-like "3.8E-11"
 void usage() {
   std::fprintf(stderr,
                "usage: tlc-hip [-config FILE.cfg] [-deadlock] [-workers N] [-gpu D] [-fpbits B]\n"
+               "               [-checkpoint MINUTES] [-metadir DIR] [-recover DIR]\n"
                "               [-tlc-order] [-no-trace] [-json] [-dump-defs] SPEC.tla\n");
 }
 
 struct Opts {
-  std::string spec, cfg;
+  std::string spec, cfg, metadir, recover;
   bool deadlock_off = false, tlc_order = false, trace = true, json = false, dump_defs = false;
   int gpu = 0, fpbits = 0;
+  double checkpoint_min = 30.0;  // TLC's default interval; 0 = never
 };
+
+// TLC's metadir name: states/yy-MM-dd-HH-mm-ss next to the spec
+std::string default_metadir(const std::string& spec) {
+  std::time_t t = std::time(nullptr);
+  char b[64];
+  std::strftime(b, sizeof b, "%y-%m-%d-%H-%M-%S", std::localtime(&t));
+  const size_t slash = spec.find_last_of('/');
+  return (slash == std::string::npos ? std::string() : spec.substr(0, slash + 1)) + "states/" + b;
+}
+
+bool make_dirs(const std::string& p) {
+  for (size_t i = 1; i <= p.size(); ++i)
+    if (i == p.size() || p[i] == '/') {
+      const std::string d = p.substr(0, i);
+      if (mkdir(d.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
+  return true;
+}
+
+const char* kCheckpointFile = "/tlcg.ckpt";
 
 // source extent of an action's definition body, for TLC's "<Action line .. of module ..>"
 std::string action_location(const Module& mod, int action) {
@@ -97,7 +121,18 @@ int main(int argc, char** argv) {
     if (a == "-config") o.cfg = next();
     else if (a == "-deadlock") o.deadlock_off = true;
     else if (a == "-workers") next();  // TLC worker threads: the GPU is the worker pool
-    else if (a == "-fp" || a == "-seed" || a == "-metadir" || a == "-fpmem") next();
+    else if (a == "-fp" || a == "-seed" || a == "-fpmem") next();
+    else if (a == "-metadir") o.metadir = next();
+    else if (a == "-recover") o.recover = next();
+    else if (a == "-checkpoint") {
+      char* end = nullptr;
+      const std::string v = next();
+      o.checkpoint_min = std::strtod(v.c_str(), &end);
+      if (v.empty() || *end || o.checkpoint_min < 0) {
+        std::fprintf(stderr, "Error: -checkpoint needs a number of minutes\n");
+        return 255;
+      }
+    }
     else if (a == "-cleanup" || a == "-nowarning" || a == "-terse") {}
     else if (a == "-gpu") o.gpu = std::atoi(next().c_str());
     else if (a == "-fpbits") o.fpbits = std::atoi(next().c_str());
@@ -145,7 +180,12 @@ int main(int argc, char** argv) {
   }
   char cerr[512];
   if (tlcg_check_model(&model, cerr, sizeof cerr) != 0) { std::printf("Error: %s\n", cerr); return 150; }
-  std::printf("Computing initial states...\n");
+  const std::string recover_file = o.recover.empty() ? "" : o.recover + kCheckpointFile;
+  if (!recover_file.empty()) {
+    std::ifstream probe(recover_file, std::ios::binary);
+    if (!probe) { std::printf("Error: cannot read checkpoint %s\n", recover_file.c_str()); return 150; }
+  }
+  if (o.metadir.empty()) o.metadir = default_metadir(o.spec);
 
   tlcg_opts opts;
   std::memset(&opts, 0, sizeof opts);
@@ -153,6 +193,7 @@ int main(int argc, char** argv) {
   opts.log2_fpset_slots = o.fpbits;
   opts.tlc_order = o.tlc_order;
   opts.world = 1;
+  if (!recover_file.empty()) opts.engine = TLCG_ENGINE_GLOBAL;  // checkpoints are global-engine level states
   tlcg_ctx* ctx = nullptr;
   if (tlcg_create(&model, &opts, &ctx) != 0) {
     std::printf("Error: %s\n", ctx ? tlcg_last_error(ctx) : "tlcg_create failed");
@@ -160,13 +201,38 @@ int main(int argc, char** argv) {
     return 255;
   }
   tlcg_stats st;
-  if (tlcg_init(ctx, &st) != 0) { std::printf("Error: %s\n", tlcg_last_error(ctx)); tlcg_destroy(ctx); return 255; }
-  std::printf("Finished computing initial states: %llu distinct state%s generated at %s.\n",
-              (unsigned long long)st.distinct, st.distinct == 1 ? "" : "s", now_str().c_str());
+  if (!recover_file.empty()) {
+    // [TLC-ext] TLC's recovery messages
+    std::printf("Starting recovery from checkpoint %s\n", o.recover.c_str());
+    if (tlcg_recover(ctx, recover_file.c_str(), &st) != 0) {
+      std::printf("Error: %s\n", tlcg_last_error(ctx));
+      tlcg_destroy(ctx);
+      return 150;
+    }
+    std::printf("Recovery completed. %llu states examined. %llu states on queue.\n",
+                (unsigned long long)(st.distinct - st.frontier), (unsigned long long)st.frontier);
+  } else {
+    std::printf("Computing initial states...\n");
+    if (tlcg_init(ctx, &st) != 0) { std::printf("Error: %s\n", tlcg_last_error(ctx)); tlcg_destroy(ctx); return 255; }
+    std::printf("Finished computing initial states: %llu distinct state%s generated at %s.\n",
+                (unsigned long long)st.distinct, st.distinct == 1 ? "" : "s", now_str().c_str());
+  }
   auto last_progress = std::chrono::steady_clock::now();
+  auto last_checkpoint = last_progress;
   while (st.status == TLCG_RUNNING) {
     if (tlcg_step_level(ctx, &st) != 0) { std::printf("Error: %s\n", tlcg_last_error(ctx)); tlcg_destroy(ctx); return 255; }
     auto now = std::chrono::steady_clock::now();
+    if (o.checkpoint_min > 0 && st.status == TLCG_RUNNING &&
+        std::chrono::duration<double>(now - last_checkpoint).count() >= 60.0 * o.checkpoint_min) {
+      // [TLC-ext] TLC's checkpoint messages; the file holds the committed levels
+      std::printf("Checkpointing of run %s\n", o.metadir.c_str());
+      if (!make_dirs(o.metadir) || tlcg_checkpoint(ctx, (o.metadir + kCheckpointFile).c_str()) != 0)
+        std::printf("Error: checkpoint failed: %s\n", tlcg_last_error(ctx));
+      else
+        std::printf("Checkpointing completed at (%s)\n", now_str().c_str());
+      std::fflush(stdout);
+      last_checkpoint = std::chrono::steady_clock::now();
+    }
     if (std::chrono::duration<double>(now - last_progress).count() > 60.0) {
       double mins = std::chrono::duration<double>(now - t0).count() / 60.0;
       std::printf("Progress(%d) at %s: %llu states generated (%.0f s/min), %llu distinct states found (%.0f ds/min), %llu states left on queue.\n",

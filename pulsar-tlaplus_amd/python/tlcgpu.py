@@ -97,6 +97,8 @@ def load_library(path: str = LIB_PATH):
         "tlcg_end_level": (C.c_int, [P, S]),
         "tlcg_outbox_read": (C.c_int, [P, I32, P, U64]),
         "tlcg_state_words": (C.c_int, [M]),
+        "tlcg_checkpoint": (C.c_int, [P, C.c_char_p]),
+        "tlcg_recover": (C.c_int, [P, C.c_char_p, S]),
         "tlcg_decode_words": (C.c_int, [M, C.POINTER(U64), C.c_char_p, I32]),
         "tlcg_host_init_state_words": (C.c_int, [M, U64, C.POINTER(U64)]),
         "tlcg_host_successors_words": (C.c_int, [M, C.POINTER(U64), C.POINTER(U64), C.POINTER(I32), I32]),
@@ -312,6 +314,15 @@ class Checker:
     def run_raw(self):
         """tlcg_run only (no host work after it): for timing."""
         self._chk(self.lib.tlcg_run(self.ctx, C.byref(self.stats)), "tlcg_run")
+        return self.stats
+
+    def checkpoint(self, path: str):
+        """TLC -checkpoint: the committed levels to `path` (global engine, between levels)."""
+        self._chk(self.lib.tlcg_checkpoint(self.ctx, path.encode()), "tlcg_checkpoint")
+
+    def recover(self, path: str):
+        """TLC -recover: resume from `path`; continue with step_level()."""
+        self._chk(self.lib.tlcg_recover(self.ctx, path.encode(), C.byref(self.stats)), "tlcg_recover")
         return self.stats
 
     def level_sizes(self) -> List[int]:

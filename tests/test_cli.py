@@ -95,5 +95,18 @@ def test_action_locations(tmp_path):
     p = subprocess.run([CLI, "-dump-defs", TLA], capture_output=True, text=True)
     assert "CompactorPhaseOne" in p.stdout
     # extents are checked through the module parser used by the trace printer
-    # via a violating run on the GPU (tests/test_gpu_cli.py); here only parsing
+    # only by a violating run on a host that has both the spec and a GPU; here only parsing
     assert re.search(r'"ASSUME", 0x[0-9a-f]{16}ull', p.stdout)
+
+
+@needs_ref
+def test_recover_needs_a_checkpoint(tmp_path):
+    # TLC -recover DIR: the checkpoint file must exist (checked before any GPU work)
+    rc, out = run_cli(tmp_path, numeric_cfg(), args=["-recover", str(tmp_path / "states" / "nope")])
+    assert "cannot read checkpoint" in out and rc == 150
+
+
+@needs_ref
+def test_checkpoint_flag_is_validated(tmp_path):
+    rc, out = run_cli(tmp_path, numeric_cfg(), args=["-checkpoint", "soon"])
+    assert "-checkpoint needs a number of minutes" in out and rc == 255
