@@ -194,6 +194,7 @@ int main(int argc, char** argv) {
   opts.tlc_order = o.tlc_order;
   opts.world = 1;
   if (!recover_file.empty()) opts.engine = TLCG_ENGINE_GLOBAL;  // checkpoints are global-engine level states
+  else std::printf("Computing initial states...\n");
   tlcg_ctx* ctx = nullptr;
   if (tlcg_create(&model, &opts, &ctx) != 0) {
     std::printf("Error: %s\n", ctx ? tlcg_last_error(ctx) : "tlcg_create failed");
@@ -212,7 +213,6 @@ int main(int argc, char** argv) {
     std::printf("Recovery completed. %llu states examined. %llu states on queue.\n",
                 (unsigned long long)(st.distinct - st.frontier), (unsigned long long)st.frontier);
   } else {
-    std::printf("Computing initial states...\n");
     if (tlcg_init(ctx, &st) != 0) { std::printf("Error: %s\n", tlcg_last_error(ctx)); tlcg_destroy(ctx); return 255; }
     std::printf("Finished computing initial states: %llu distinct state%s generated at %s.\n",
                 (unsigned long long)st.distinct, st.distinct == 1 ? "" : "s", now_str().c_str());
