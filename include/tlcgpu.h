@@ -192,6 +192,12 @@ int tlcg_host_check_invariants_words(const tlcg_model* m, const uint64_t* state)
  * only.  Returns the states compared (0: the component engine does not take
  * this model), or < 0 on a disagreement. */
 int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint64_t n);
+/* PROPERTY Termination (compaction.tla:303-307).  Spec has no fairness, so a
+ * behavior may stutter forever in its initial state: <>P fails iff an
+ * initial state violates P.  Returns the first such initial state (TLC Init
+ * order; the counterexample is that state followed by stuttering), -1 when
+ * the property holds, < -1 on a bad model. */
+int64_t tlcg_host_termination_counterexample(const tlcg_model* m);
 /* Owner rank of a state under the context's partition. */
 int tlcg_owner(tlcg_ctx* c, uint64_t state);
 

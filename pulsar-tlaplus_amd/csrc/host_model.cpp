@@ -374,6 +374,23 @@ int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state) {
   return check_invariants(hm.L, state);
 }
 
+// PROPERTY Termination == <>(Len(messages) = MessageSentLimit /\
+// compactorState = Compactor_In_PhaseTwoWrite /\ MaxCompactedLedgerId = ... /\
+// (ModelConsumer => ...)), compaction.tla:303-307: its body is the guard of
+// Terminating (:205-213), terminating_enabled.  Spec == Init /\ [][Next]_vars
+// (:233) has no fairness, so every behavior may stutter forever in its initial
+// state: <>P is violated iff some initial state has ~P, and the behavior
+// "that state, then stuttering" is a counterexample.  Returns the first such
+// initial state in TLC's Init order, or -1 when every initial state satisfies P.
+int64_t tlcg_host_termination_counterexample(const tlcg_model* m) {
+  HostModel hm;
+  std::string e;
+  if (!m || !build_model(*m, &hm, &e)) return -2;
+  for (u64 i = 0; i < hm.n_init; ++i)
+    if (!terminating_enabled(hm.L, init_state<u128>(hm.L, i))) return (int64_t)i;
+  return -1;
+}
+
 // Component-specialized evaluators (component_model.h) vs the generic ones
 // (model.h) on every state of the components of initial states
 // [first, first + n): the compactor successor, the stutter count and the

@@ -505,9 +505,15 @@ bool bind_model(const Config& cfg, const Module& mod, bool deadlock_flag, tlcg_m
     *err = "Error: the configuration needs SPECIFICATION Spec or INIT Init / NEXT Next.";
     return false;
   }
-  if (!cfg.properties.empty()) {
-    *err = "Error: temporal PROPERTY checking (e.g. Termination) is not supported by this checker.";
-    return false;
+  for (auto& name : cfg.properties) {
+    if (!mod.find(name)) {
+      *err = "Error: The property " + name + " specified in the configuration file is not defined in the specification.";
+      return false;
+    }
+    if (name != "Termination" || !invariant_matches(mod, name)) {
+      *err = "Error: temporal property " + name + " is not one this checker implements (Termination as published).";
+      return false;
+    }
   }
   m->msg_sent_limit = (int32_t)msl;
   m->compaction_times_limit = (int32_t)ctl;

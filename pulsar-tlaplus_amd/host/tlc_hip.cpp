@@ -242,7 +242,25 @@ int main(int argc, char** argv) {
     }
   }
   int rc = 0;
-  if (st.status == TLCG_DONE) {
+  // PROPERTY Termination, checked like TLC after the safety search of the
+  // complete state space ([TLC-ext] message text)
+  int64_t live_idx = -1;
+  if (st.status == TLCG_DONE && !cfg.properties.empty()) {
+    std::printf("Checking temporal properties for the complete state space with %llu total distinct states at (%s)\n",
+                (unsigned long long)st.distinct, now_str().c_str());
+    live_idx = tlcg_host_termination_counterexample(&model);
+  }
+  if (live_idx >= 0) {
+    uint64_t s0[2] = {0, 0};
+    std::vector<char> buf(1 << 16);
+    tlcg_host_init_state_words(&model, (uint64_t)live_idx, s0);
+    tlcg_decode_words(&model, s0, buf.data(), (int32_t)buf.size());
+    std::printf("Error: Temporal properties were violated.\n\n");
+    std::printf("Error: The following behavior constitutes a counter-example:\n\n");
+    std::printf("State 1: <Initial predicate>\n%s\n\n", buf.data());
+    std::printf("State 2: Stuttering\n");
+    rc = 13;
+  } else if (st.status == TLCG_DONE) {
     std::printf("Model checking completed. No error has been found.\n");
     std::printf("  Estimates of the probability that TLC did not check all reachable states\n");
     std::printf("  because two distinct states had the same fingerprint:\n");

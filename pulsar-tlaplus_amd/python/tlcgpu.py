@@ -89,6 +89,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_host_successors": (C.c_int, [M, U64, C.POINTER(U64), C.POINTER(I32), I32]),
         "tlcg_host_check_invariants": (C.c_int, [M, U64]),
         "tlcg_host_component_selfcheck": (C.c_int64, [M, U64, U64]),
+        "tlcg_host_termination_counterexample": (C.c_int64, [M]),
         "tlcg_owner": (C.c_int, [P, U64]),
         "tlcg_expand": (C.c_int, [P, S]),
         "tlcg_outbox": (C.c_int, [P, I32, C.POINTER(P), C.POINTER(U64)]),

@@ -30,12 +30,15 @@ def numeric_cfg(**over):
              KeySpace="{1, 2}", ValueSpace="{1, 2}", RetainNullKey="TRUE", MaxCrashTimes="1", ModelProducer="FALSE")
     c.update(over)
     inv = c.pop("INVARIANTS", "TypeSafe, CompactionHorizonCorrectness")
+    prop = c.pop("PROPERTY", None)
     body = "\nCONSTANTS\n" + ",\n".join(f"    {k} = {v}" for k, v in c.items() if v is not None)
     mvs = ["Nil", "Compactor_In_PhaseOne", "Compactor_In_PhaseTwoWrite", "Compactor_In_PhaseTwoUpdateContext",
            "Compactor_In_PhaseTwoUpdateHorizon", "Compactor_In_PhaseTwoPersistCusror",
            "Compactor_In_PhaseTwoDeleteLedger"]
     body += "\n\nCONSTANTS\n" + ",\n".join(f"    {m} = {m}" for m in mvs)
     body += "\n\n(* a block (* nested *) comment *)\nSPECIFICATION Spec\n\nINVARIANTS\n    " + inv + "\n    \\* done\n"
+    if prop:
+        body += "\nPROPERTY " + prop + "\n"
     return body
 
 
@@ -65,6 +68,8 @@ def test_numeric_twin_reaches_the_gpu(tmp_path):
     (dict(MaxCrashTimes=None), "The constant parameter MaxCrashTimes is not assigned a value", 150),
     (dict(INVARIANTS="TypeSafe, NoSuchInvariant"), "NoSuchInvariant specified in the configuration file is not defined", 150),
     (dict(INVARIANTS="Termination"), "not one this checker implements", 150),
+    (dict(PROPERTY="TypeSafe"), "temporal property TypeSafe is not one this checker implements", 150),
+    (dict(PROPERTY="NoSuchProperty"), "The property NoSuchProperty specified in the configuration file is not defined", 150),
 ])
 def test_cfg_errors(tmp_path, over, expect, code):
     rc, out = run_cli(tmp_path, numeric_cfg(**over))
@@ -110,3 +115,10 @@ def test_recover_needs_a_checkpoint(tmp_path):
 def test_checkpoint_flag_is_validated(tmp_path):
     rc, out = run_cli(tmp_path, numeric_cfg(), args=["-checkpoint", "soon"])
     assert "-checkpoint needs a number of minutes" in out and rc == 255
+
+
+@needs_ref
+def test_termination_property_is_accepted(tmp_path):
+    # PROPERTY Termination (compaction.tla:303-307) is checked after the safety search
+    rc, out = run_cli(tmp_path, numeric_cfg(PROPERTY="Termination"))
+    assert "Computing initial states..." in out

@@ -4,6 +4,8 @@ libtlcgpu.so -- the same code the gfx950 kernels run) against the oracle.
 A plain Python BFS over tlcg_host_successors must reproduce the golden counts,
 per-level sizes and traces; decoded trace states must match the oracle's TLC
 text byte for byte.  No GPU call is made."""
+import ctypes
+
 import pytest
 
 import tlcgpu
@@ -115,3 +117,25 @@ def test_component_specialization_matches_generic(case):
     n = tlcgpu.host_component_selfcheck(m, 0, 300)
     bits = tlcgpu.load_library().tlcg_state_bits(m.to_c())
     assert n > 0 or (n == 0 and bits > 32), n
+
+
+@pytest.mark.parametrize("case", ["S", "P_published", "S_consumer", "W_C12_k1", "D_N0_K0", "X_empty_spaces"])
+def test_termination_counterexample(case):
+    """PROPERTY Termination: Spec has no fairness, so <>P fails iff an initial
+    state violates P (the behavior: that state, then stuttering).  The first
+    such state in Init order, against the Python oracle's P."""
+    import oracle_py
+    c = GOLDEN[case]["constants"]
+    m = model_of(c)
+    py = oracle_py.Model(N=c["N"], C=c["C"], K=c["K"], keys=c["keys"], values=c["values"], retain=c["retain"],
+                         producer=c["producer"], consumer=c["consumer"], ctl=c["ctl"])
+
+    def p(s):  # the body of Termination, compaction.tla:303-307
+        msgs, led, cur, ph, p1r, hz, ctx, crash, cons = s
+        return (len(msgs) == c["N"] and ph == oracle_py.W and py.max_ledger(led) == c["C"]
+                and (not c["consumer"] or cons == c["ctl"]))
+    want = next((i for i, s in enumerate(py.inits()) if not p(s)), -1)
+    lib = tlcgpu.load_library()
+    lib.tlcg_host_termination_counterexample.restype = ctypes.c_int64
+    got = lib.tlcg_host_termination_counterexample(ctypes.byref(m.to_c()))
+    assert got == want == 0  # every initial state is in PhaseOne (compaction.tla:199)
