@@ -27,6 +27,9 @@ CONFIGS = {
     "s": dict(keys=2, distinct=45_198, generated=60_507, depth=20),
     # CompactionTimesLimit = 12, a 93-bit (two-word) state
     "g9deep": dict(keys=10, C=12, distinct=986_759_477, generated=1_119_626_552, depth=74),
+    # an open state space: the producer modelled (no components; every level
+    # crosses ranks at N > 1), oracle-pinned in tests/golden/p8.json
+    "p8": dict(keys=7, producer=True, retain=False, distinct=91_781_506, generated=161_341_378, depth=23),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic bytes per distinct state of the fused expand kernel:
@@ -63,7 +66,9 @@ def model_for(cfg):
     import tlcgpu
     k = CONFIGS[cfg]["keys"]
     return tlcgpu.Model(key_space=range(1, k + 1), value_space=range(1, k + 1),
-                        compaction_times_limit=CONFIGS[cfg].get("C", 3))
+                        compaction_times_limit=CONFIGS[cfg].get("C", 3),
+                        model_producer=CONFIGS[cfg].get("producer", False),
+                        retain_null_key=CONFIGS[cfg].get("retain", True))
 
 
 def algorithmic_bytes(distinct, generated, n_init, selfloops, words=1):
@@ -91,16 +96,31 @@ def selfloops_per_m(model):
 
 def cpu_baseline(cfg, seconds_target=12.0):
     """The oracle (TEST INFRASTRUCTURE, single thread) on a bounded sample of the
-    same workload: the first n initial message sequences of the cfg."""
+    same workload: the first n initial message sequences of the cfg (for a
+    producer-modelled cfg, which has one initial state: the whole check of the
+    same spec at KeySpace = ValueSpace = {1..4})."""
     oracle = os.path.join(ROOT, "oracle", "build", "tlc_oracle")
     if not os.path.exists(oracle):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
-    k = CONFIGS[cfg]["keys"]
+    c = CONFIGS[cfg]
+    if c.get("producer"):
+        keys = "1,2,3,4"
+        t = time.time()
+        out = subprocess.run([oracle, "-keys", keys, "-values", keys, "-producer", "1", "-retain",
+                              "0" if c.get("retain") is False else "1", "-notrace"],
+                             check=True, capture_output=True, text=True).stdout
+        r = json.loads(out)
+        return dict(value=r["distinct"] / r["seconds"], unit="distinct states/s", cores=1, kind="port",
+                    sample=f"oracle/tlc_oracle (C restatement, 1 thread), the whole producer-modelled check at "
+                           f"KeySpace = ValueSpace = {{1..4}}: {r['distinct']} distinct states in "
+                           f"{r['seconds']:.2f} s (TLC itself is not installed on the GPU host)",
+                    wall_s=round(time.time() - t, 2))
+    k = c["keys"]
     keys = ",".join(str(i) for i in range(1, k + 1))
     n_m = 4096
     while True:
         t = time.time()
-        out = subprocess.run([oracle, "-keys", keys, "-values", keys, "-C", str(CONFIGS[cfg].get("C", 3)),
+        out = subprocess.run([oracle, "-keys", keys, "-values", keys, "-C", str(c.get("C", 3)),
                               "-init-lo", "0", "-init-hi", str(n_m),
                               "-notrace"], check=True, capture_output=True, text=True).stdout
         wall = time.time() - t
@@ -190,16 +210,17 @@ def main():
         return dict(engine=used, jit=jit, elapsed=elapsed, expand_ms=ems / args.steps, kernel_ms=kms / args.steps,
                     launches=launches)
 
-    def time_exchange():
-        """BASELINE config 4: the global engine with the FPSet hash-partitioned on
-        the whole state (partition 2), so successors cross ranks and every BFS
-        level runs expand -> all-to-all of {state, parent} records (RCCL over
-        xGMI) -> absorb -> all-reduce (dist.run)."""
+    def time_exchange(partition):
+        """The global engine with successors crossing ranks, so every BFS level
+        runs expand -> all-to-all of {state, parent} records (RCCL over xGMI) ->
+        absorb -> all-reduce (dist.run).  BASELINE config 4: on G9 the FPSet is
+        partitioned on the whole state (partition 2); a producer-modelled cfg
+        is open by itself (partition 0)."""
         per_rank = cfg["distinct"] // world + 1
         log2 = max(16, (2 * per_rank - 1).bit_length())
         cap = int(per_rank * 1.1) + (1 << 20)
         eng = tdist.GpuEngine(model, rank, world, gpu, log2_fpset_slots=log2, state_capacity=cap, engine="global",
-                              partition=2)
+                              partition=partition)
         assert not eng.closed
         for _ in range(args.warmup):
             tdist.run(eng, dev=rdev)
@@ -207,37 +228,45 @@ def main():
         dist.barrier()
         torch.cuda.synchronize(dev)
         timing = {}
-        k0 = eng.stats.kernel_ms
+        kms = ems = 0.0
         t0 = time.perf_counter()
         for _ in range(args.steps):
             r = tdist.run(eng, dev=rdev, timing=timing)
+            kms += r.kernel_ms
+            ems += r.expand_ms
         torch.cuda.synchronize(dev)
         dist.barrier()
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
-        t = torch.tensor([elapsed, timing.get("exchange_s", 0.0)], dtype=torch.float64, device=rdev)
+        t = torch.tensor([elapsed, timing.get("exchange_s", 0.0), ems, kms], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         eng.close()
         if (r.generated, r.distinct, r.depth) != (cfg["generated"], cfg["distinct"], cfg["depth"]):
             raise SystemExit(f"count mismatch (exchange): {(r.generated, r.distinct, r.depth)} want {cfg}")
-        return dict(engine="global", partition="whole state (owner = mix64(state))",
+        return dict(engine="global", jit=0, elapsed=float(t[0]), expand_ms=float(t[2]) / args.steps,
+                    kernel_ms=float(t[3]) / args.steps, launches=cfg["depth"] - 1,
+                    partition="whole state (owner = mix64(state))" if partition == 2 else "open (Producer)",
                     exchange="all_to_all_single per level, " + dist.get_backend(),
-                    value=round(cfg["distinct"] * args.steps / float(t[0]), 1),
-                    ms_per_step=round(float(t[0]) * 1e3 / args.steps, 3),
                     exchange_ms_per_step=round(float(t[1]) * 1e3 / args.steps, 3))
 
-    main_run = time_engine("auto")
-    global_run = time_engine("global")
-    exchange_run = None
-    if distributed and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
-        exchange_run = time_exchange()
+    open_model = bool(cfg.get("producer"))
+    exchange_run = global_run = None
+    if open_model and distributed:
+        main_run = time_exchange(0)  # successors leave their rank: the exchange is the path
+    else:
+        main_run = time_engine("auto")
+        global_run = time_engine("global") if not open_model else None
+        if distributed and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
+            exchange_run = time_exchange(2)
     if rank != 0:
         if distributed:
             dist.destroy_process_group()
         return
     distinct, generated = cfg["distinct"], cfg["generated"]
-    n_init = (cfg["keys"] + 1) ** 6
-    selfloops = n_init * selfloops_per_m(model)
+    # (a producer-modelled cfg has one initial state; its Terminating stutters
+    # are not counted out of the probes, so its bytes/state is an upper bound)
+    n_init = 1 if open_model else (cfg["keys"] + 1) ** 6
+    selfloops = 0 if open_model else n_init * selfloops_per_m(model)
 
     def roofline_global(r):
         abytes = algorithmic_bytes(distinct, generated, n_init, selfloops, words)
@@ -245,7 +274,8 @@ def main():
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                  kernel="k_expand_fast" if words == 1 else "k_expand<u128> (wide FPSet)",
+                  kernel=("k_expand_fast" if words == 1 and not open_model else
+                          "k_expand<u64, Producer>" if words == 1 else "k_expand<u128> (wide FPSet)"),
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
                   bytes_per_distinct=round(abytes / distinct, 2))
         pmc = load_profile(PMC_PROFILE)
@@ -285,12 +315,16 @@ def main():
         return rf
 
     def summary(r):
-        return dict(engine=r["engine"], jit=bool(r["jit"]), value=round(distinct * args.steps / r["elapsed"], 1),
-                    ms_per_step=round(r["elapsed"] * 1e3 / args.steps, 3),
-                    gpu_kernel_ms_per_step=round(r["kernel_ms"], 3),
-                    roofline=roofline_component(r) if r["engine"] == "component" else roofline_global(r))
+        out = dict(engine=r["engine"], jit=bool(r["jit"]), value=round(distinct * args.steps / r["elapsed"], 1),
+                   ms_per_step=round(r["elapsed"] * 1e3 / args.steps, 3),
+                   gpu_kernel_ms_per_step=round(r["kernel_ms"], 3),
+                   roofline=roofline_component(r) if r["engine"] == "component" else roofline_global(r))
+        for k in ("partition", "exchange", "exchange_ms_per_step"):
+            if k in r:
+                out[k] = r[k]
+        return out
 
-    main_s, glob_s = summary(main_run), summary(global_run)
+    main_s = summary(main_run)
     line = {
         "metric": "distinct states/sec, compaction.tla scaled cfg, 1/2/4/8 MI355X vs host TLC",
         "value": main_s["value"],
@@ -306,16 +340,19 @@ def main():
         "data": "synthetic: the model's own state space (no external data)",
         "config": {"workload": f"compaction.tla BFS, {args.config.upper()} cfg: KeySpace = ValueSpace = "
                                f"{{1..{cfg['keys']}}}, MessageSentLimit 3, CompactionTimesLimit {cfg.get('C', 3)}, "
-                               f"MaxCrashTimes 1, RetainNullKey, no producer/consumer",
+                               f"MaxCrashTimes 1, RetainNullKey {'FALSE' if cfg.get('retain') is False else 'TRUE'}, "
+                               f"{'ModelProducer' if open_model else 'no producer'}, no consumer",
                    "state_bits": tlcgpu.state_bits(model),
                    "distinct": distinct, "generated": generated, "depth": cfg["depth"],
                    "parallelism": f"partition{world}", "engine": main_s["engine"],
                    "gpu_kernel_ms_per_step": main_s["gpu_kernel_ms_per_step"]},
         "roofline": main_s["roofline"],
-        "engines": {"global_hbm_fpset": glob_s},
+        "engines": {},
     }
+    if global_run:
+        line["engines"]["global_hbm_fpset"] = summary(global_run)
     if exchange_run:
-        line["engines"]["global_open_partition_alltoall"] = exchange_run
+        line["engines"]["global_open_partition_alltoall"] = summary(exchange_run)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config)
     print(json.dumps(line), flush=True)

@@ -223,3 +223,17 @@ def test_g9deep_scaled_counts():
     assert (r.distinct, r.generated, r.depth) == (986_759_477, 1_119_626_552, 74)
     assert r.engine == "global"
 
+
+
+def test_p8_producer_scaled_matches_oracle():
+    """An open (producer-modelled) state space of ~1e8 states on the global
+    engine: KeySpace = ValueSpace = 1..7, ModelProducer, RetainNullKey FALSE;
+    counts and every level against the C oracle (tests/golden/p8.json)."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "p8.json")))
+    r = tlcgpu.run(model_of(g["constants"]))
+    want = g["result"]
+    assert r.engine == "global" and r.status == "ok"
+    assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                            want["levels"])
