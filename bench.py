@@ -245,6 +245,7 @@ def main():
             raise SystemExit(f"count mismatch (exchange): {(r.generated, r.distinct, r.depth)} want {cfg}")
         return dict(engine="global", jit=0, elapsed=float(t[0]), expand_ms=float(t[2]) / args.steps,
                     kernel_ms=float(t[3]) / args.steps, launches=cfg["depth"] - 1,
+                    kernel="k_expand<u64, open partition> + k_absorb",
                     partition="whole state (owner = mix64(state))" if partition == 2 else "open (Producer)",
                     exchange="all_to_all_single per level, " + dist.get_backend(),
                     exchange_ms_per_step=round(float(t[1]) * 1e3 / args.steps, 3))
@@ -274,8 +275,9 @@ def main():
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                  kernel=("k_expand_fast" if words == 1 and not open_model else
-                          "k_expand<u64, Producer>" if words == 1 else "k_expand<u128> (wide FPSet)"),
+                  kernel=r.get("kernel") or ("k_expand_fast" if words == 1 and not open_model else
+                                             "k_expand<u64, Producer>" if words == 1 else
+                                             "k_expand<u128> (wide FPSet)"),
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
                   bytes_per_distinct=round(abytes / distinct, 2))
         pmc = load_profile(PMC_PROFILE)
