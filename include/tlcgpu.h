@@ -215,6 +215,9 @@ int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st);
  * or device) copied in and absorbed.  The raw tlcg_outbox/tlcg_inbox pointers
  * need the caller to order its own copies against the context's stream. */
 int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n);
+/* All destinations' records in rank order, contiguous (the all-to-all send
+ * buffer; sum of the tlcg_outbox counts x 16 bytes), one stream sync. */
+int tlcg_outbox_gather(tlcg_ctx* c, void* out);
 int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats* st);
 
 /* TLC -checkpoint: write the run's committed levels (state store + parent

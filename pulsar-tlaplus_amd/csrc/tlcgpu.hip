@@ -1783,6 +1783,25 @@ int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n) {
   return 0;
 }
 
+// Every destination's records, destination-major in rank order (this rank's
+// own, always empty, skipped), copied to one caller buffer with one stream
+// synchronization: the send buffer of an all-to-all.
+int tlcg_outbox_gather(tlcg_ctx* c, void* out) {
+  if (!c) return -1;
+  u64 off = 0;
+  for (int dst = 0; dst < c->opts.world; ++dst) {
+    if (dst == c->opts.rank) continue;
+    const u64 n = c->h_ctr->n_out[dst];
+    if (!n) continue;
+    if (!c->d_outbox || n > c->outbox_cap) return -1;
+    HIPCHK_I(hipMemcpyAsync((char*)out + off * 16, c->d_outbox + 2 * (u64)dst * c->outbox_cap, n * 16,
+                            hipMemcpyDefault, c->stream));
+    off += n;
+  }
+  HIPCHK_I(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 // tlcg_inbox + copy + tlcg_absorb in one call: the copy of the caller's
 // records (host or device) and the insert run in order on the context's stream.
 int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats* st) {

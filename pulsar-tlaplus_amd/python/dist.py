@@ -80,6 +80,16 @@ class GpuEngine:
                          "tlcg_outbox_read")
         return t
 
+    def outbox_all(self, counts: List[int], device) -> torch.Tensor:
+        """Every destination's records, destination-major (the all-to-all send
+        buffer), gathered by the library with one stream synchronization."""
+        t = torch.empty((sum(counts), 2), dtype=torch.int64, device=device)
+        if t.shape[0]:
+            if t.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.ck._chk(self.lib.tlcg_outbox_gather(self.ctx, C.c_void_p(t.data_ptr())), "tlcg_outbox_gather")
+        return t
+
     def absorb(self, recs: torch.Tensor):
         """Insert records from other ranks (device or host tensor, [n, 2] int64)."""
         recs = recs.contiguous()
@@ -161,13 +171,11 @@ def run(engine, group=None, dev: Optional[torch.device] = None, timing: Optional
         dist.all_to_all_single(recv_counts, send_counts, group=group)
         rc = [int(x) for x in recv_counts.tolist()]
         sc = [int(x) for x in send_counts.tolist()]
-        sends = [engine.outbox(d) if sc[d] else None for d in range(world)]
-        send = torch.empty((sum(sc), 2), dtype=torch.int64, device=xdev)
-        off = 0
-        for d in range(world):
-            if sends[d] is not None:
-                send[off:off + sc[d]].copy_(sends[d])
-                off += sc[d]
+        if hasattr(engine, "outbox_all"):
+            send = engine.outbox_all(sc, xdev)
+        else:  # per-destination stand-in engines (tests)
+            send = torch.cat([engine.outbox(d) if sc[d] else torch.empty((0, 2), dtype=torch.int64)
+                              for d in range(world)], 0).to(xdev)
         recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=xdev)
         dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc, group=group)
         xs += time.perf_counter() - t0

@@ -97,6 +97,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_absorb": (C.c_int, [P, U64, S]),
         "tlcg_end_level": (C.c_int, [P, S]),
         "tlcg_outbox_read": (C.c_int, [P, I32, P, U64]),
+        "tlcg_outbox_gather": (C.c_int, [P, P]),
         "tlcg_state_words": (C.c_int, [M]),
         "tlcg_checkpoint": (C.c_int, [P, C.c_char_p]),
         "tlcg_recover": (C.c_int, [P, C.c_char_p, S]),
