@@ -139,13 +139,28 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
   auto emit = [&](bool pred, W t, u64 dkey) {
     bool isnew = false;
     u64 slot = 0;
-    if (pred) {
-      bool local = true;
-      if (PART) {
-        const int dst = owner_of(t, a.owner_mask, a.world);
-        if (dst != a.rank) {
-          local = false;
-          const unsigned long long pos = atomicAdd(&a.ctr->n_out[dst], 1ull);
+    bool local = pred;
+    if (PART) {
+      // successors owned elsewhere go to that rank's outbox.  The wave claims
+      // room with one atomic per destination, issued together by lanes
+      // 0..world-1 (a per-lane atomic on the world's few n_out words would
+      // serialize at the memory side)
+      const int dst = pred ? owner_of(t, a.owner_mask, a.world) : a.rank;
+      const bool remote = dst != a.rank;
+      local = pred && !remote;
+      if (__ballot(remote)) {
+        const int lane = __lane_id();
+        u64 mine = 0;  // lane d: the lanes sending to destination d
+        for (int d = 0; d < a.world; ++d) {
+          const u64 m = __ballot(remote && dst == d);
+          if (lane == d) mine = m;
+        }
+        unsigned long long base = 0;
+        if (mine) base = atomicAdd(&a.ctr->n_out[lane], (unsigned long long)__popcll(mine));
+        const u64 m = __shfl((unsigned long long)mine, dst);
+        base = __shfl(base, dst);
+        if (remote) {
+          const unsigned long long pos = base + (unsigned long long)__popcll(m & lanemask_lt());
           if (pos < a.outbox_cap) {
             u64* rec = a.outbox + 2 * ((u64)dst * a.outbox_cap + pos);
             rec[0] = (u64)t;  // PART: one-word states only (tlcg_create)
@@ -155,15 +170,15 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
           }
         }
       }
-      if (local) {
-        const int r = fpset_put(a.slots, a.log2, t, mixw(t), &slot);
-        if (r < 0) atomicOr(&a.ctr->overflow, ovf_of(r));
-        isnew = r == 1;
-        if (TLC && r >= 0) atomicMin((unsigned long long*)&a.dkey_slot[slot], (unsigned long long)dkey);
-        if (!TLC && isnew) {
-          const int c = check_invariants(L, t);
-          if (c >= 0) ev = min(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
-        }
+    }
+    if (local) {
+      const int r = fpset_put(a.slots, a.log2, t, mixw(t), &slot);
+      if (r < 0) atomicOr(&a.ctr->overflow, ovf_of(r));
+      isnew = r == 1;
+      if (TLC && r >= 0) atomicMin((unsigned long long*)&a.dkey_slot[slot], (unsigned long long)dkey);
+      if (!TLC && isnew) {
+        const int c = check_invariants(L, t);
+        if (c >= 0) ev = min(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
       }
     }
     stage_append<TLC, W>(isnew, t, a.rank_tag | dkey, slot, s_st, s_par, s_slot, &s_cnt);

@@ -16,7 +16,7 @@ from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libtlcgpu.so"))
+LIB_PATH = os.environ.get("TLCG_LIB") or os.path.normpath(os.path.join(HERE, "..", "lib", "libtlcgpu.so"))
 
 MAX_SET = 63
 MAX_INV = 8
