@@ -195,7 +195,7 @@ def main():
         elapsed = time.perf_counter() - t0
         counts = [st.generated, st.distinct]
         used = tlcgpu.ENGINE_NAMES.get(int(st.engine), "?")
-        jit = int(st.reserved[0])
+        jit = int(st.jit_used)
         launches = len(eng.level_sizes()) if used == "global" else 1
         if distributed:
             t = torch.tensor([elapsed, ems, kms], dtype=torch.float64, device=rdev)

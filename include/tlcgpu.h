@@ -100,7 +100,14 @@ typedef struct tlcg_opts {
   int32_t rank, world;       /* fingerprint partition: this context owns rank of world */
   int32_t partition;         /* 0 auto (by `messages` when it is immutable), 1 by `messages`, 2 whole state */
   int32_t engine;            /* TLCG_ENGINE_*: 0 auto, 1 global HBM FPSet, 2 component (closed partitions) */
-  int32_t reserved[6];
+  /* Global engine: move committed levels other than the frontier (states and
+   * parent log, the trace) to pinned host memory instead of growing the
+   * device state store past device_store_cap states (0: past what free HBM
+   * allows).  TLC spills its trace and queue to disk the same way
+   * (StateQueue, TLCTrace); counts, levels and traces are unchanged. */
+  int32_t spill;
+  uint64_t device_store_cap;
+  int32_t reserved[4];
 } tlcg_opts;
 
 /* BFS engines.  GLOBAL: level-synchronous BFS over one HBM FPSet (64-bit CAS),
@@ -125,7 +132,9 @@ typedef struct tlcg_stats {
   double expand_ms;          /* device time of the expand kernels alone */
   uint64_t levels_redone;    /* levels re-run after an FPSet / store growth */
   uint64_t engine;           /* TLCG_ENGINE_* that produced these numbers */
-  uint64_t reserved[3];
+  uint64_t jit_used;         /* 1: the layout-specialized (hipRTC) component kernels ran */
+  uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
+  uint64_t reserved[1];
 } tlcg_stats;
 
 typedef struct tlcg_ctx tlcg_ctx;

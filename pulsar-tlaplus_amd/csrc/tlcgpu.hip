@@ -17,6 +17,9 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <chrono>
+#include <thread>
+#include <sys/mman.h>
 
 #include "component.h"
 #include "host_model.h"
@@ -479,7 +482,23 @@ struct tlcg_ctx {
   // state store (all levels) + parent log
   u64* d_states = nullptr;
   u64* d_parents = nullptr;
-  u64 cap = 0;
+  u64 cap = 0;  // device slots; they hold the states with gidx in [win, win + cap)
+  // host spill (opts.spill): committed states below `win` live in pinned host
+  // chunks, each a gidx range [g0, g0 + n) of states and parent refs
+  struct HostChunk {
+    u64 g0, n;
+    u64* st;
+    u64* par;
+  };
+  std::vector<HostChunk> hchunks;
+  u64 win = 0;
+  // registered host blocks not in use (kept for the next run; freed by tlcg_destroy)
+  struct HostBlock {
+    void* p;
+    size_t bytes;
+  };
+  std::vector<HostBlock> host_pool;
+  std::vector<std::pair<void*, size_t>> host_sizes;  // every registered block
   // TLC-order scratch
   u64* d_slot_new = nullptr;
   u64* d_dk = nullptr;
@@ -562,9 +581,81 @@ namespace {
   } while (0)
 
 u64 distinct_of(const tlcg_ctx* c) { return c->level_base.empty() ? 0 : c->level_base.back(); }
+// device address of the state / parent ref with global index g (g >= win)
+u64* dev_state(tlcg_ctx* c, u64 g) { return c->d_states + (g - c->win) * c->words; }
+u64* dev_parent(tlcg_ctx* c, u64 g) { return c->d_parents + (g - c->win); }
+// device slots from global index g to the end of the store
+u64 dev_room(const tlcg_ctx* c, u64 g) { return c->cap - (g - c->win); }
 // first unused slot of the state store
 u64 store_end(const tlcg_ctx* c) {
   return c->engine == TLCG_ENGINE_COMPONENT ? c->comp_store_used : distinct_of(c);
+}
+
+// Pinned host memory for spilled levels.  hipHostMalloc pins 4 KiB pages one
+// by one (0.23 s/GiB to allocate, 0.16 s/GiB to free on the MI355X box,
+// profiles/r01_pin_probe.jsonl); an anonymous mapping backed by transparent
+// huge pages, zeroed by a few threads and then registered with HIP, is ready
+// 30x sooner and copies at the same 57 GB/s.  Blocks are pooled across runs.
+void* host_block(tlcg_ctx* c, size_t bytes) {
+  bytes = (bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+  size_t best = c->host_pool.size();
+  for (size_t i = 0; i < c->host_pool.size(); ++i)
+    if (c->host_pool[i].bytes >= bytes && (best == c->host_pool.size() || c->host_pool[i].bytes < c->host_pool[best].bytes))
+      best = i;
+  if (best < c->host_pool.size()) {
+    void* p = c->host_pool[best].p;
+    c->host_pool.erase(c->host_pool.begin() + (long)best);
+    return p;
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+  madvise(p, bytes, MADV_HUGEPAGE);
+  const unsigned hw = std::thread::hardware_concurrency();
+  const size_t nt = std::max<size_t>(1, std::min<size_t>({16, hw ? hw : 1, bytes >> 26}));
+  std::vector<std::thread> th;
+  const size_t per = (bytes / nt + 4095) & ~(size_t)4095;
+  for (size_t i = 0; i < nt; ++i)
+    th.emplace_back([=] {
+      const size_t off = i * per;
+      if (off < bytes) std::memset((char*)p + off, 0, std::min(per, bytes - off));
+    });
+  for (auto& t : th) t.join();
+  if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
+    munmap(p, bytes);
+    return nullptr;
+  }
+  c->host_sizes.emplace_back(p, bytes);
+  return p;
+}
+
+size_t host_block_bytes(const tlcg_ctx* c, void* p) {
+  for (const auto& b : c->host_sizes)
+    if (b.first == p) return b.second;
+  return 0;
+}
+
+// back to the pool (the next run reuses it)
+void host_release(tlcg_ctx* c, void* p) {
+  if (p) c->host_pool.push_back({p, host_block_bytes(c, p)});
+}
+
+void free_host_chunks(tlcg_ctx* c) {
+  for (auto& h : c->hchunks) {
+    host_release(c, h.st);
+    host_release(c, h.par);
+  }
+  c->hchunks.clear();
+  c->win = 0;
+}
+
+void destroy_host_pool(tlcg_ctx* c) {
+  free_host_chunks(c);
+  for (const auto& b : c->host_pool) {
+    hipHostUnregister(b.p);
+    munmap(b.p, b.bytes);
+  }
+  c->host_pool.clear();
+  c->host_sizes.clear();
 }
 
 bool alloc_bytes(tlcg_ctx* c, void** p, size_t bytes, const char* what) {
@@ -580,20 +671,72 @@ bool alloc_bytes(tlcg_ctx* c, void** p, size_t bytes, const char* what) {
   return true;
 }
 
-// grow the state store so that it holds `need` states (keeps contents)
-bool ensure_store(tlcg_ctx* c, u64 need) {
-  if (need <= c->cap) return true;
-  u64 ncap = std::max<u64>(need + need / 4, c->cap * 2);
-  ncap = std::max<u64>(ncap, 1u << 16);
-  size_t fr = 0, tot = 0;
-  if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
-    u64 room = (u64)(fr * 0.9) / (8 * (c->words + 1)) + c->cap;  // both arrays; old ones freed after copy
-    if (ncap > room && need <= room) ncap = room;
+// Spill: move the committed states [win, f0) -- every level below the
+// frontier -- to a pinned host chunk, and slide [f0, end) to the start of the
+// device store.  Between kernels only (synchronous).
+bool spill_below(tlcg_ctx* c, u64 f0, u64 end) {
+  const u64 n = f0 - c->win, w = c->words;
+  tlcg_ctx::HostChunk h{c->win, n, nullptr, nullptr};
+  const bool tr = std::getenv("TLCG_SPILL_TRACE") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  h.st = (u64*)host_block(c, n * 8 * w);
+  h.par = h.st ? (u64*)host_block(c, n * 8) : nullptr;
+  if (!h.par) {
+    host_release(c, h.st);
+    char b[160];
+    std::snprintf(b, sizeof b, "out of pinned host memory spilling %llu states (%.2f GiB)", (unsigned long long)n,
+                  n * 8.0 * (w + 1) / 1073741824.0);
+    c->err = b;
+    return false;
   }
+  const double t_alloc = ms();
+  HIPCHK(hipMemcpyAsync(h.st, c->d_states, n * 8 * w, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(h.par, c->d_parents, n * 8, hipMemcpyDeviceToHost, c->stream));
+  // pieces of at most n states: source and destination never overlap
+  for (u64 off = 0; off < end - f0; off += n) {
+    const u64 m = std::min<u64>(n, end - f0 - off);
+    HIPCHK(hipMemcpyAsync(c->d_states + off * w, c->d_states + (n + off) * w, m * 8 * w, hipMemcpyDeviceToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_parents + off, c->d_parents + n + off, m * 8, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (tr)
+    std::fprintf(stderr, "spill: %llu states, alloc %.1f ms, copies %.1f ms\n", (unsigned long long)n, t_alloc,
+                 ms() - t_alloc);
+  c->hchunks.push_back(h);
+  c->win = f0;
+  return true;
+}
+
+// grow the state store so that it holds the states up to global index `need`
+// (keeps contents); with opts.spill, first spill the levels below the frontier
+// when the store would outgrow its budget
+bool ensure_store(tlcg_ctx* c, u64 need) {
+  if (need - c->win <= c->cap) return true;
+  // in use: [win, end) (nothing while a recover loads the store)
+  const u64 end = std::max<u64>(c->win, std::min<u64>(c->win + c->cap, store_end(c) + c->pending));
+  size_t fr = 0, tot = 0;
+  const bool have_fr = hipMemGetInfo(&fr, &tot) == hipSuccess;
+  // states the device could hold: free memory (both arrays, old ones freed after the copy) + what it holds
+  const u64 room = have_fr ? (u64)(fr * 0.9) / (8 * (c->words + 1)) + c->cap : ~0ull;
+  const u64 budget = c->opts.spill && c->opts.device_store_cap ? std::min<u64>(room, c->opts.device_store_cap) : room;
+  if (c->opts.spill && c->engine == TLCG_ENGINE_GLOBAL && c->level_base.size() >= 2 && need - c->win > budget) {
+    const u64 f0 = c->level_base[c->level_base.size() - 2];  // first state of the frontier
+    // worth a pass when it frees at least 1/16 of what stays (bounds the slide's pieces)
+    if (f0 > c->win && (f0 - c->win) * 16 >= end - f0) {
+      if (!spill_below(c, f0, end)) return false;
+      if (need - c->win <= c->cap) return true;
+    }
+  }
+  const u64 dn = need - c->win;
+  u64 ncap = std::max<u64>(dn + dn / 4, c->cap * 2);
+  ncap = std::max<u64>(ncap, 1u << 16);
+  if (ncap > budget && dn <= budget) ncap = budget;
   u64 *ns = nullptr, *np = nullptr;
   if (!alloc_bytes(c, (void**)&ns, ncap * 8 * c->words, "state store")) return false;
   if (!alloc_bytes(c, (void**)&np, ncap * 8, "parent log")) { hipFree(ns); return false; }
-  const u64 keep = std::min<u64>(c->cap, store_end(c) + c->pending);
+  const u64 keep = end - c->win;
   if (keep) {
     HIPCHK(hipMemcpyAsync(ns, c->d_states, keep * 8 * c->words, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(np, c->d_parents, keep * 8, hipMemcpyDeviceToDevice, c->stream));
@@ -623,13 +766,36 @@ bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
   if (c->d_dkey_slot) HIPCHK(hipMemsetAsync(c->d_dkey_slot, 0xFF, 8ull << log2, c->stream));
   if (n) {
     HIPCHK(hipMemsetAsync(c->d_aux, 0, sizeof(LevelCtr), c->stream));
-    if (c->words == 1)
-      k_reinsert<u64><<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(c->d_states, n, c->d_slots, log2,
-                                                                               c->d_aux);
-    else
-      k_reinsert<u128><<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>((const u128*)c->d_states, n,
-                                                                                c->d_slots, log2, c->d_aux);
-    HIPCHK(hipGetLastError());
+    auto reinsert = [&](const u64* dev, u64 m) {
+      if (c->words == 1)
+        k_reinsert<u64><<<grid_for(m, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(dev, m, c->d_slots, log2, c->d_aux);
+      else
+        k_reinsert<u128><<<grid_for(m, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>((const u128*)dev, m, c->d_slots,
+                                                                                  log2, c->d_aux);
+      return hipGetLastError() == hipSuccess;
+    };
+    if (!c->hchunks.empty()) {  // spilled states pass through a device staging buffer
+      const u64 stage_n = 1u << 22;
+      u64* stage = nullptr;
+      if (!alloc_bytes(c, (void**)&stage, stage_n * 8 * c->words, "FPSet rebuild staging")) return false;
+      bool ok = true;
+      for (const auto& h : c->hchunks)
+        for (u64 off = 0; ok && off < h.n; off += stage_n) {
+          const u64 m = std::min<u64>(stage_n, h.n - off);
+          ok = hipMemcpyAsync(stage, h.st + off * c->words, m * 8 * c->words, hipMemcpyHostToDevice, c->stream) ==
+                   hipSuccess &&
+               reinsert(stage, m) && hipStreamSynchronize(c->stream) == hipSuccess;
+        }
+      hipFree(stage);
+      if (!ok) {
+        c->err = "FPSet rebuild from host memory failed";
+        return false;
+      }
+    }
+    if (n > c->win && !reinsert(c->d_states, n - c->win)) {
+      c->err = "FPSet rebuild launch failed";
+      return false;
+    }
     HIPCHK(hipMemcpyAsync(c->h_aux, c->d_aux, sizeof(LevelCtr), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (c->h_aux->overflow) {
@@ -699,7 +865,8 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
                       : (depth ? c->level_base[(size_t)depth] - c->level_base[(size_t)depth - 1] : 0);
   st->depth = depth;
   st->engine = (uint64_t)c->engine;
-  st->reserved[0] = c->jit_used ? 1 : 0;  // layout-specialized kernels ran
+  st->jit_used = c->jit_used ? 1 : 0;
+  st->host_states = c->win;
   st->status = c->status;
   st->invariant = -1;
   st->action = -1;
@@ -716,10 +883,23 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   st->levels_redone = c->levels_redone;
 }
 
+// the host chunk holding spilled state g (< win)
+const tlcg_ctx::HostChunk& chunk_of(const tlcg_ctx* c, u64 g) {
+  auto it = std::upper_bound(c->hchunks.begin(), c->hchunks.end(), g,
+                             [](u64 x, const tlcg_ctx::HostChunk& h) { return x < h.g0; });
+  return *(it - 1);
+}
+
 bool state_at(tlcg_ctx* c, u64 g, u128* s, u64* p) {
   uint64_t w[2] = {0, 0};
-  HIPCHK(hipMemcpy(w, c->d_states + g * c->words, 8 * c->words, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(p, c->d_parents + g, 8, hipMemcpyDeviceToHost));
+  if (g < c->win) {
+    const auto& h = chunk_of(c, g);
+    std::memcpy(w, h.st + (g - h.g0) * c->words, 8 * c->words);
+    *p = h.par[g - h.g0];
+  } else {
+    HIPCHK(hipMemcpy(w, dev_state(c, g), 8 * c->words, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(p, dev_parent(c, g), 8, hipMemcpyDeviceToHost));
+  }
   *s = join_words(w, c->words);
   return true;
 }
@@ -1055,15 +1235,15 @@ bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
   const Layout& L = c->hm.L;
   ExpandArgs a;
   a.L = L;
-  a.frontier = c->d_states + front0 * c->words;
+  a.frontier = dev_state(c, front0);
   a.n_front = n_front;
   a.front_gidx0 = front0;
   a.slots = c->d_slots;
   a.log2 = c->log2;
   const u64 d = distinct_of(c);
-  a.states_out = c->d_states + d * c->words;
-  a.parents_out = c->d_parents + d;
-  a.cap_out = c->cap - d;
+  a.states_out = dev_state(c, d);
+  a.parents_out = dev_parent(c, d);
+  a.cap_out = dev_room(c, d);
   a.slot_out = c->d_slot_new;
   a.dkey_slot = c->d_dkey_slot;
   a.ctr = c->d_ctr;
@@ -1119,15 +1299,15 @@ bool tlc_order_level(tlcg_ctx* c, u64 n_new) {
   const unsigned g = grid_for(n_new, BLOCK, 0x7fffffffu);
   const u64 tag = (u64)c->opts.rank << 56;
   if (c->words == 1) {
-    HIPCHK_I(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, c->d_states + d, c->d_st2,
+    HIPCHK_I(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, dev_state(c, d), c->d_st2,
                                                 (int)n_new, 0, end_bit, c->stream));
-    k_tlc_finish<u64><<<g, BLOCK, 0, c->stream>>>(L, n_new, c->d_st2, c->d_dk2, c->d_states + d, c->d_parents + d,
+    k_tlc_finish<u64><<<g, BLOCK, 0, c->stream>>>(L, n_new, c->d_st2, c->d_dk2, dev_state(c, d), dev_parent(c, d),
                                                   tag, c->d_ctr);
   } else {
-    u128* st = (u128*)c->d_states + d;
+    u128* st = (u128*)dev_state(c, d);
     HIPCHK_I(hipcub::DeviceRadixSort::SortPairs(c->d_sort_tmp, tmp, c->d_dk, c->d_dk2, (const u128*)st,
                                                 (u128*)c->d_st2, (int)n_new, 0, end_bit, c->stream));
-    k_tlc_finish<u128><<<g, BLOCK, 0, c->stream>>>(L, n_new, (const u128*)c->d_st2, c->d_dk2, st, c->d_parents + d,
+    k_tlc_finish<u128><<<g, BLOCK, 0, c->stream>>>(L, n_new, (const u128*)c->d_st2, c->d_dk2, st, dev_parent(c, d),
                                                    tag, c->d_ctr);
   }
   HIPCHK_I(hipGetLastError());
@@ -1163,7 +1343,7 @@ bool step_level(tlcg_ctx* c) {
   const u64 est = next_level_estimate(c, F);
   if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return false;
   if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + est)) return false;
-  if (!ensure_scratch(c, std::min(worst, c->cap - d))) return false;
+  if (!ensure_scratch(c, std::min(worst, dev_room(c, d)))) return false;
   for (;;) {
     if (!reset_ctr(c)) return false;
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
@@ -1190,8 +1370,8 @@ bool step_level(tlcg_ctx* c) {
     // grow and redo the level from the committed levels
     ++c->levels_redone;
     if (ovf & OVF_STORE) {
-      if (!ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * (c->cap - d)))) return false;
-      if (!ensure_scratch(c, c->cap - d)) return false;
+      if (!ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * dev_room(c, d)))) return false;
+      if (!ensure_scratch(c, dev_room(c, d))) return false;
     }
     if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d)) return false;
   }
@@ -1281,6 +1461,7 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_dkey_slot);
   hipFree(c->d_states);
   hipFree(c->d_parents);
+  destroy_host_pool(c);
   hipFree(c->d_slot_new);
   hipFree(c->d_dk);
   hipFree(c->d_dk2);
@@ -1310,6 +1491,7 @@ void* tlcg_stream(tlcg_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
   if (!c || !c->stream) return -1;
+  free_host_chunks(c);
   c->kernel_ms = c->expand_ms = 0;
   c->status = TLCG_RUNNING;
   c->ev_word = NO_EVENT;
@@ -1396,7 +1578,16 @@ int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_
 
 int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
   if (!c || first + n > store_end(c)) return -1;
-  if (n && hipMemcpy(out, c->d_states + first * c->words, n * 8 * c->words, hipMemcpyDeviceToHost) != hipSuccess) {
+  const u64 w = c->words;
+  while (n && first < c->win) {  // spilled states
+    const auto& h = chunk_of(c, first);
+    const u64 m = std::min<u64>(n, h.g0 + h.n - first);
+    std::memcpy(out, h.st + (first - h.g0) * w, m * 8 * w);
+    out += m * w;
+    first += m;
+    n -= m;
+  }
+  if (n && hipMemcpy(out, dev_state(c, first), n * 8 * w, hipMemcpyDeviceToHost) != hipSuccess) {
     c->err = "copy failed";
     return -10;
   }
@@ -1578,8 +1769,11 @@ int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
   bool ok = hipHostMalloc(&stage, kStage) == hipSuccess;
   ok = ok && std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(&c->model, sizeof c->model, 1, f) == 1 &&
        std::fwrite(c->level_base.data(), 8, c->level_base.size(), f) == c->level_base.size();
-  ok = ok && dev_to_file(c, f, c->d_states, d * 8 * c->words, stage) &&
-       dev_to_file(c, f, c->d_parents, d * 8, stage);
+  // spilled levels from their host chunks, the rest from the device
+  for (const auto& hc : c->hchunks) ok = ok && std::fwrite(hc.st, 8 * c->words, hc.n, f) == hc.n;
+  ok = ok && dev_to_file(c, f, c->d_states, (d - c->win) * 8 * c->words, stage);
+  for (const auto& hc : c->hchunks) ok = ok && std::fwrite(hc.par, 8, hc.n, f) == hc.n;
+  ok = ok && dev_to_file(c, f, c->d_parents, (d - c->win) * 8, stage);
   if (stage) hipHostFree(stage);
   ok = (std::fclose(f) == 0) && ok;
   if (!ok || std::rename(tmp.c_str(), path) != 0) {
@@ -1623,14 +1817,36 @@ int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
   c->passes.clear();
   c->level_base.clear();
   c->pending = 0;
-  const u64 d = h.distinct;
+  c->err.clear();
+  free_host_chunks(c);
+  const u64 d = h.distinct, w = c->words;
+  // with opts.spill the levels below the frontier go straight to host memory
+  const u64 f0 = c->opts.spill && lb.size() >= 2 ? lb[lb.size() - 2] : 0;
+  tlcg_ctx::HostChunk hc{0, f0, nullptr, nullptr};
   void* stage = nullptr;
-  bool ok = hipHostMalloc(&stage, kStage) == hipSuccess && ensure_store(c, d + (d >> 3) + (1u << 16));
-  ok = ok && file_to_dev(c, f, c->d_states, d * 8 * c->words, stage) &&
-       file_to_dev(c, f, c->d_parents, d * 8, stage);
+  bool ok = hipHostMalloc(&stage, kStage) == hipSuccess;
+  if (ok && f0) {
+    hc.st = (u64*)host_block(c, f0 * 8 * w);
+    hc.par = hc.st ? (u64*)host_block(c, f0 * 8) : nullptr;
+    ok = hc.par != nullptr;
+    if (!ok) {
+      host_release(c, hc.st);
+      c->err = "out of pinned host memory for the spilled levels";
+    } else {
+      c->hchunks.push_back(hc);
+      c->win = f0;
+    }
+  }
+  const u64 dn = d - f0;
+  ok = ok && ensure_store(c, d + (dn >> 3) + (1u << 16));
+  ok = ok && (!f0 || std::fread(hc.st, 8 * w, f0, f) == f0) && file_to_dev(c, f, c->d_states, dn * 8 * w, stage) &&
+       (!f0 || std::fread(hc.par, 8, f0, f) == f0) && file_to_dev(c, f, c->d_parents, dn * 8, stage);
   if (stage) hipHostFree(stage);
   std::fclose(f);
-  if (!ok) return -10;
+  if (!ok) {
+    if (c->err.empty()) c->err = "checkpoint file is truncated";
+    return -10;
+  }
   c->level_base = lb;
   c->generated = h.generated;
   c->levels_redone = h.levels_redone;
@@ -1719,7 +1935,7 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
       for (int r = 0; r < c->opts.world; ++r) mx = std::max<u64>(mx, c->h_ctr->n_out[r]);
       per_dst = std::max<u64>(2 * per_dst, mx + mx / 4);
     }
-    if ((ovf & OVF_STORE) && !ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * (c->cap - d)))) return -10;
+    if ((ovf & OVF_STORE) && !ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * dev_room(c, d)))) return -10;
     if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d)) return -10;
   }
   c->generated += c->h_ctr->generated;
@@ -1764,7 +1980,7 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
   for (;;) {
     if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
     k_absorb<<<grid_for(n_records, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
-        c->hm.L, c->d_inbox, n_records, c->d_slots, c->log2, c->d_states + d, c->d_parents + d, c->cap - d,
+        c->hm.L, c->d_inbox, n_records, c->d_slots, c->log2, dev_state(c, d), dev_parent(c, d), dev_room(c, d),
         c->d_ctr);
     if (hipGetLastError() != hipSuccess) return -10;
     if (hipEventRecord(c->e1, c->stream) != hipSuccess) return -10;

@@ -193,6 +193,9 @@ int main(int argc, char** argv) {
   opts.log2_fpset_slots = o.fpbits;
   opts.tlc_order = o.tlc_order;
   opts.world = 1;
+  // like TLC's disk-backed trace and queue: committed levels move to host
+  // memory when HBM runs short (never otherwise)
+  opts.spill = 1;
   if (!recover_file.empty()) opts.engine = TLCG_ENGINE_GLOBAL;  // checkpoints are global-engine level states
   else std::printf("Computing initial states...\n");
   tlcg_ctx* ctx = nullptr;

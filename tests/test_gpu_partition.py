@@ -12,8 +12,8 @@ from conftest import GOLDEN, model_of
 pytestmark = pytest.mark.gpu
 
 
-def run_virtual(model, world, partition=0):
-    engines = [tdist.GpuEngine(model, r, world, 0, partition=partition) for r in range(world)]
+def run_virtual(model, world, partition=0, **opts):
+    engines = [tdist.GpuEngine(model, r, world, 0, partition=partition, **opts) for r in range(world)]
     try:
         if engines[0].closed:
             stats = [e.run_closed() for e in engines]
