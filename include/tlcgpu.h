@@ -107,7 +107,15 @@ typedef struct tlcg_opts {
    * (StateQueue, TLCTrace); counts, levels and traces are unchanged. */
   int32_t spill;
   uint64_t device_store_cap;
-  int32_t reserved[4];
+  /* Host FPSet tier (TLC's DiskFPSet), global engine, <= 63-bit states: when
+   * the HBM FPSet would grow past 2^log2_fpset_max slots (0: past what free
+   * HBM allows), the states it holds move to a sorted run in host memory,
+   * summarized in HBM by a blocked Bloom filter, and the HBM table restarts
+   * empty.  Each level's new states are checked against the host runs where
+   * the filter says "maybe".  Counts, levels and traces are unchanged. */
+  int32_t fpset_spill;
+  int32_t log2_fpset_max;
+  int32_t reserved[2];
 } tlcg_opts;
 
 /* BFS engines.  GLOBAL: level-synchronous BFS over one HBM FPSet (64-bit CAS),
@@ -134,7 +142,7 @@ typedef struct tlcg_stats {
   uint64_t engine;           /* TLCG_ENGINE_* that produced these numbers */
   uint64_t jit_used;         /* 1: the layout-specialized (hipRTC) component kernels ran */
   uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
-  uint64_t reserved[1];
+  uint64_t fpset_host_states; /* states held by the host FPSet tier (tlcg_opts.fpset_spill) */
 } tlcg_stats;
 
 typedef struct tlcg_ctx tlcg_ctx;

@@ -415,6 +415,69 @@ __global__ __launch_bounds__(BLOCK) void k_reinsert(const W* __restrict__ states
   if (r < 0) atomicOr(&ctr->overflow, ovf_of(r));
 }
 
+// ---- host FPSet tier (opts.fpset_spill).  The host runs hold the mixed keys
+// mix64(state) (a bijection, so exact) in sorted order; HBM holds a blocked
+// Bloom filter over them: 2^log2b blocks of 64 bytes, 6 bits per key.
+__device__ __forceinline__ u64 bloom_hash(u64 key) { return mix64(key ^ 0x5851F42D4C957F2Dull); }
+
+__global__ __launch_bounds__(BLOCK) void k_bloom_insert(const u64* __restrict__ keys, u64 n, u64* __restrict__ bloom,
+                                                        int log2b) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const u64 h = bloom_hash(keys[i]);
+  u64* b = bloom + 8 * (h >> (64 - log2b));
+  const u64 h2 = mix64(h);
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const unsigned bit = (unsigned)(h2 >> (9 * j)) & 511u;
+    atomicOr((unsigned long long*)&b[bit >> 6], 1ull << (bit & 63));
+  }
+}
+
+// the level's new states [0, n) (new to the HBM table): queue the ones the
+// filter cannot rule out of the host runs as {mixed key, position}
+__global__ __launch_bounds__(BLOCK) void k_tier_filter(const u64* __restrict__ states, u64 n,
+                                                       const u64* __restrict__ bloom, int log2b, u64* __restrict__ q_key,
+                                                       u64* __restrict__ q_pos, unsigned long long* q_n) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  bool maybe = false;
+  u64 key = 0;
+  if (i < n) {
+    key = mix64(states[i]);
+    const u64 h = bloom_hash(key);
+    const u64* b = bloom + 8 * (h >> (64 - log2b));
+    const u64 h2 = mix64(h);
+    maybe = true;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const unsigned bit = (unsigned)(h2 >> (9 * j)) & 511u;
+      maybe = maybe && ((b[bit >> 6] >> (bit & 63)) & 1);
+    }
+  }
+  const u64 m = __ballot(maybe);
+  if (!m) return;
+  unsigned long long base = 0;
+  if (__lane_id() == __ffsll((unsigned long long)m) - 1) base = atomicAdd(q_n, (unsigned long long)__popcll(m));
+  base = __shfl(base, __ffsll((unsigned long long)m) - 1);
+  if (maybe) {
+    const u64 p = base + __popcll(m & lanemask_lt());
+    q_key[p] = key;
+    q_pos[p] = i;
+  }
+}
+
+// keep[pos] = 0 for the queued states the host runs hold
+__global__ __launch_bounds__(BLOCK) void k_tier_mark(const u64* __restrict__ q_pos, const unsigned char* __restrict__ dup,
+                                                     u64 m, unsigned char* __restrict__ keep) {
+  const u64 j = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (j < m && dup[j]) keep[q_pos[j]] = 0;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_mix_keys(const u64* __restrict__ states, u64 n, u64* __restrict__ keys) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (i < n) keys[i] = mix64(states[i]);
+}
+
 // ---- world > 1: insert successors received from other ranks
 __global__ __launch_bounds__(BLOCK) void k_absorb(Layout L, const u64* __restrict__ recs, u64 n,
                                                   u64* __restrict__ slots, int log2, u64* __restrict__ states_out,
@@ -499,6 +562,27 @@ struct tlcg_ctx {
   };
   std::vector<HostBlock> host_pool;
   std::vector<std::pair<void*, size_t>> host_sizes;  // every registered block
+  // host FPSet tier (opts.fpset_spill): the states [0, t0_base) are held by
+  // sorted runs of mixed keys in host memory (one per flush) and summarized by
+  // an HBM Bloom filter; the HBM table holds the states from t0_base on
+  struct Run {
+    u64* keys;
+    u64 n;
+  };
+  std::vector<Run> runs;
+  u64 t0_base = 0;
+  u64* d_bloom = nullptr;
+  int bloom_log2 = 0;  // 2^bloom_log2 blocks of 64 bytes
+  // level filter scratch (grown on demand)
+  u64* d_q = nullptr;  // [2][cap]: queued keys, positions (then sorted copies)
+  unsigned char* d_keep = nullptr;
+  u64* d_sel = nullptr;  // selected states / parents
+  void* d_ftmp = nullptr;
+  size_t ftmp_bytes = 0;
+  u64 filt_cap = 0;
+  unsigned long long* d_qn = nullptr;
+  u64 tier_queued = 0, tier_dups = 0;  // filter "maybe"s, and the ones the host runs held
+  double tier_ms[4] = {0, 0, 0, 0};     // flush, Bloom filter pass, host lookups, compaction (wall)
   // TLC-order scratch
   u64* d_slot_new = nullptr;
   u64* d_dk = nullptr;
@@ -571,6 +655,15 @@ namespace {
     }                                                                             \
   } while (0)
 // the same for the int-returning entry points (< 0 = error)
+#define HIPCHK_U(expr)                                                            \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      c->err = std::string(#expr) + ": " + hipGetErrorString(_e);                 \
+      return ~0ull;                                                               \
+    }                                                                             \
+  } while (0)
+
 #define HIPCHK_I(expr)                                                            \
   do {                                                                            \
     hipError_t _e = (expr);                                                       \
@@ -586,6 +679,13 @@ u64* dev_state(tlcg_ctx* c, u64 g) { return c->d_states + (g - c->win) * c->word
 u64* dev_parent(tlcg_ctx* c, u64 g) { return c->d_parents + (g - c->win); }
 // device slots from global index g to the end of the store
 u64 dev_room(const tlcg_ctx* c, u64 g) { return c->cap - (g - c->win); }
+// the host chunk holding spilled state g (< win)
+const tlcg_ctx::HostChunk& chunk_of(const tlcg_ctx* c, u64 g) {
+  auto it = std::upper_bound(c->hchunks.begin(), c->hchunks.end(), g,
+                             [](u64 x, const tlcg_ctx::HostChunk& h) { return x < h.g0; });
+  return *(it - 1);
+}
+
 // first unused slot of the state store
 u64 store_end(const tlcg_ctx* c) {
   return c->engine == TLCG_ENGINE_COMPONENT ? c->comp_store_used : distinct_of(c);
@@ -750,7 +850,41 @@ bool ensure_store(tlcg_ctx* c, u64 need) {
   return true;
 }
 
-// (re)build the FPSet at 2^log2 slots holding states[0, n)
+// Calls fn(dev, m) on the stored states [g0, g1) in order, m at a time: the
+// device window in place, spilled ranges through a device staging buffer.
+// fn enqueues on the context's stream and returns false on a launch error.
+template <typename F>
+bool for_each_stored(tlcg_ctx* c, u64 g0, u64 g1, F&& fn) {
+  const u64 w = c->words;
+  const u64 e = std::min(g1, c->win);
+  if (g0 < e) {
+    const u64 stage_n = 1u << 22;
+    u64* stage = nullptr;
+    if (!alloc_bytes(c, (void**)&stage, stage_n * 8 * w, "host-store staging")) return false;
+    bool ok = true;
+    for (u64 g = g0; ok && g < e;) {
+      const auto& h = chunk_of(c, g);
+      const u64 m = std::min<u64>(std::min<u64>(stage_n, e - g), h.g0 + h.n - g);
+      ok = hipMemcpyAsync(stage, h.st + (g - h.g0) * w, m * 8 * w, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+           fn((const u64*)stage, m) && hipStreamSynchronize(c->stream) == hipSuccess;
+      g += m;
+    }
+    hipFree(stage);
+    if (!ok) {
+      c->err = "reading spilled states back failed";
+      return false;
+    }
+  }
+  const u64 a = std::max(g0, c->win);
+  if (a < g1 && !fn((const u64*)dev_state(c, a), g1 - a)) {
+    c->err = "kernel launch failed";
+    return false;
+  }
+  return true;
+}
+
+// (re)build the FPSet at 2^log2 slots holding the stored states [t0_base, n)
+// (with the host FPSet tier, older states are in the host runs)
 bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
   if (log2 != c->log2 || !c->d_slots) {
     hipFree(c->d_slots);
@@ -764,7 +898,7 @@ bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
   }
   HIPCHK(hipMemsetAsync(c->d_slots, 0, (8ull * c->words) << log2, c->stream));
   if (c->d_dkey_slot) HIPCHK(hipMemsetAsync(c->d_dkey_slot, 0xFF, 8ull << log2, c->stream));
-  if (n) {
+  if (n > c->t0_base) {
     HIPCHK(hipMemsetAsync(c->d_aux, 0, sizeof(LevelCtr), c->stream));
     auto reinsert = [&](const u64* dev, u64 m) {
       if (c->words == 1)
@@ -774,28 +908,7 @@ bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
                                                                                   log2, c->d_aux);
       return hipGetLastError() == hipSuccess;
     };
-    if (!c->hchunks.empty()) {  // spilled states pass through a device staging buffer
-      const u64 stage_n = 1u << 22;
-      u64* stage = nullptr;
-      if (!alloc_bytes(c, (void**)&stage, stage_n * 8 * c->words, "FPSet rebuild staging")) return false;
-      bool ok = true;
-      for (const auto& h : c->hchunks)
-        for (u64 off = 0; ok && off < h.n; off += stage_n) {
-          const u64 m = std::min<u64>(stage_n, h.n - off);
-          ok = hipMemcpyAsync(stage, h.st + off * c->words, m * 8 * c->words, hipMemcpyHostToDevice, c->stream) ==
-                   hipSuccess &&
-               reinsert(stage, m) && hipStreamSynchronize(c->stream) == hipSuccess;
-        }
-      hipFree(stage);
-      if (!ok) {
-        c->err = "FPSet rebuild from host memory failed";
-        return false;
-      }
-    }
-    if (n > c->win && !reinsert(c->d_states, n - c->win)) {
-      c->err = "FPSet rebuild launch failed";
-      return false;
-    }
+    if (!for_each_stored(c, c->t0_base, n, reinsert)) return false;
     HIPCHK(hipMemcpyAsync(c->h_aux, c->d_aux, sizeof(LevelCtr), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (c->h_aux->overflow) {
@@ -806,13 +919,332 @@ bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
   return true;
 }
 
-// keep the FPSet load <= 1/2 for `need` states; re-inserts the stored ones
-// (committed levels + what the current level appended so far)
+// ---- host FPSet tier (opts.fpset_spill; TLC's DiskFPSet) ----
+
+double wall_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// largest HBM table: the option, else what free memory allows
+int fpset_max_log2(tlcg_ctx* c) {
+  if (c->opts.log2_fpset_max > 0) return c->opts.log2_fpset_max;
+  if (c->opts.log2_fpset_slots > 0) return c->opts.log2_fpset_slots;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 40;
+  const u64 avail = (u64)(fr * 0.8) + (c->d_slots ? (8ull * c->words) << c->log2 : 0);
+  const u64 per_slot = 8ull * c->words + (c->opts.tlc_order ? 8 : 0);
+  int l = 16;
+  while (l < 40 && (per_slot << (l + 1)) <= avail) ++l;
+  return l;
+}
+
+void free_tier(tlcg_ctx* c) {
+  for (auto& r : c->runs) host_release(c, r.keys);
+  c->runs.clear();
+  c->t0_base = 0;
+  c->tier_queued = c->tier_dups = 0;
+  for (double& t : c->tier_ms) t = 0;
+  if (c->d_bloom) (void)hipMemsetAsync(c->d_bloom, 0, 64ull << c->bloom_log2, c->stream);
+}
+
+// insert every host run's keys into a (new) Bloom filter of 2^log2b blocks
+bool bloom_rebuild(tlcg_ctx* c, int log2b) {
+  u64* nb = nullptr;
+  if (!alloc_bytes(c, (void**)&nb, 64ull << log2b, "FPSet tier Bloom filter")) return false;
+  hipFree(c->d_bloom);
+  c->d_bloom = nb;
+  c->bloom_log2 = log2b;
+  HIPCHK(hipMemsetAsync(c->d_bloom, 0, 64ull << log2b, c->stream));
+  const u64 stage_n = 1u << 24;
+  u64* stage = nullptr;
+  bool ok = true;
+  for (const auto& r : c->runs)
+    for (u64 off = 0; ok && off < r.n; off += stage_n) {
+      if (!stage && !alloc_bytes(c, (void**)&stage, stage_n * 8, "Bloom staging")) return false;
+      const u64 m = std::min<u64>(stage_n, r.n - off);
+      ok = hipMemcpyAsync(stage, r.keys + off, m * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+      k_bloom_insert<<<grid_for(m, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(stage, m, c->d_bloom, log2b);
+      ok = ok && hipGetLastError() == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+    }
+  hipFree(stage);
+  if (!ok) c->err = "Bloom filter rebuild failed";
+  return ok;
+}
+
+// Merge every host run into one sorted run (lookups cost a search per run).
+// Keys are uniform on [0, 2^64): thread t merges the key range
+// [t, t + 1) * 2^64 / T of all runs into its own slice of the output.
+constexpr size_t kMaxRuns = 16;
+
+bool merge_runs(tlcg_ctx* c) {
+  u64 total = 0;
+  for (const auto& r : c->runs) total += r.n;
+  u64* out = (u64*)host_block(c, total * 8);
+  if (!out) {
+    c->err = "out of host memory merging the FPSet tier";
+    return false;
+  }
+  const unsigned hw = std::thread::hardware_concurrency();
+  const u64 nt = std::max<u64>(1, std::min<u64>(16, hw ? hw : 1));
+  const size_t R = c->runs.size();
+  // cut[t][r]: first index of run r in thread t's key range
+  std::vector<std::vector<u64>> cut(nt + 1, std::vector<u64>(R));
+  for (u64 t = 0; t <= nt; ++t)
+    for (size_t r = 0; r < R; ++r) {
+      const auto& run = c->runs[r];
+      cut[t][r] = t == nt ? run.n
+                          : t == 0 ? 0
+                                   : (u64)(std::lower_bound(run.keys, run.keys + run.n,
+                                                            (u64)(((unsigned __int128)t << 64) / nt)) - run.keys);
+    }
+  auto work = [&](u64 t) {
+    u64 o = 0;
+    for (size_t r = 0; r < R; ++r) o += cut[t][r];
+    u64* base = out + o;
+    u64 len = 0;
+    for (size_t r = 0; r < R; ++r) {  // append run r's piece, then merge it into what is there
+      const u64 a = cut[t][r], b = cut[t + 1][r];
+      std::memcpy(base + len, c->runs[r].keys + a, (b - a) * 8);
+      std::inplace_merge(base, base + len, base + len + (b - a));
+      len += b - a;
+    }
+  };
+  std::vector<std::thread> th;
+  for (u64 t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& t : th) t.join();
+  for (auto& r : c->runs) host_release(c, r.keys);
+  c->runs.assign(1, tlcg_ctx::Run{out, total});
+  return true;
+}
+
+// Move the stored states [t0_base, g1) out of the HBM table into a new
+// sorted host run.  The sort reuses the table's own memory (the table is
+// rebuilt right after): keys and their alternate buffer fit in its 8 * 2^log2
+// bytes because its load is <= 1/2.
+bool flush_tier(tlcg_ctx* c, u64 g1) {
+  const u64 n = g1 - c->t0_base;
+  if (!n) return true;
+  const double t0 = wall_ms();
+  struct Acc {
+    double& a;
+    double t0;
+    ~Acc() { a += wall_ms() - t0; }
+  } acc{c->tier_ms[0], t0};
+  const u64 half = (1ull << c->log2) / 2;
+  if (!c->d_slots || n > half) {
+    c->err = "internal: FPSet tier flush larger than the table";
+    return false;
+  }
+  u64* keys = c->d_slots;
+  u64* alt = c->d_slots + half;
+  u64 off = 0;
+  auto mix = [&](const u64* dev, u64 m) {
+    k_mix_keys<<<grid_for(m, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(dev, m, keys + off);
+    off += m;
+    return hipGetLastError() == hipSuccess;
+  };
+  if (!for_each_stored(c, c->t0_base, g1, mix)) return false;
+  hipcub::DoubleBuffer<u64> db(keys, alt);
+  size_t tmp = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, db, (int)n, 0, 64, c->stream));
+  void* d_tmp = nullptr;
+  if (!alloc_bytes(c, &d_tmp, tmp, "FPSet tier sort scratch")) return false;
+  const hipError_t e = hipcub::DeviceRadixSort::SortKeys(d_tmp, tmp, db, (int)n, 0, 64, c->stream);
+  tlcg_ctx::Run r{(u64*)host_block(c, n * 8), n};
+  bool ok = e == hipSuccess && r.keys &&
+            hipMemcpyAsync(r.keys, db.Current(), n * 8, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+            hipStreamSynchronize(c->stream) == hipSuccess;
+  if (!ok) {
+    hipFree(d_tmp);
+    host_release(c, r.keys);
+    c->err = r.keys ? "FPSet tier flush failed" : "out of host memory for the FPSet tier";
+    return false;
+  }
+  // the Bloom filter: 16+ bits per host-tier state, doubled ahead of need;
+  // a resize re-inserts the older runs from host memory, the new run's keys
+  // go in from the device copy still at hand
+  int lb = std::max(c->bloom_log2, 10);
+  while ((512ull << lb) < 16 * g1) ++lb;
+  if (lb != c->bloom_log2 || !c->d_bloom) {
+    hipFree(d_tmp);
+    d_tmp = nullptr;
+    if (!bloom_rebuild(c, std::min(lb + 1, 40))) {
+      host_release(c, r.keys);
+      return false;
+    }
+  }
+  k_bloom_insert<<<grid_for(n, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(db.Current(), n, c->d_bloom,
+                                                                           c->bloom_log2);
+  ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+  hipFree(d_tmp);
+  if (!ok) {
+    host_release(c, r.keys);
+    c->err = "Bloom filter insert failed";
+    return false;
+  }
+  c->runs.push_back(r);
+  c->t0_base = g1;
+  return c->runs.size() <= kMaxRuns || merge_runs(c);
+}
+
+// first index in [from, n) whose key is >= key, galloping from `from`
+inline u64 gallop_lb(const u64* k, u64 n, u64 from, u64 key) {
+  if (from >= n || k[from] >= key) return from;
+  u64 lo = from, step = 1;  // k[lo] < key
+  while (lo + step < n && k[lo + step] < key) {
+    lo += step;
+    step <<= 1;
+  }
+  return (u64)(std::lower_bound(k + lo + 1, k + std::min<u64>(n, lo + step + 1), key) - k);
+}
+
+// dup[j] = 1 iff the host runs hold key q[j].  The queries are sorted, so
+// each thread merges its slice against every run, galloping forward: the
+// runs are streamed, not probed at random.  Up to 16 threads.
+void host_tier_lookup(const tlcg_ctx* c, const u64* q, u64 m, unsigned char* dup) {
+  const unsigned hw = std::thread::hardware_concurrency();
+  const u64 nt = std::max<u64>(1, std::min<u64>(std::min<u64>(16, hw ? hw : 1), m / 4096 + 1));
+  auto work = [&](u64 a, u64 b) {
+    std::memset(dup + a, 0, b - a);
+    for (const auto& r : c->runs) {
+      u64 pos = (u64)(std::lower_bound(r.keys, r.keys + r.n, q[a]) - r.keys);
+      for (u64 j = a; j < b && pos < r.n; ++j) {
+        if (dup[j]) continue;
+        pos = gallop_lb(r.keys, r.n, pos, q[j]);
+        if (pos < r.n && r.keys[pos] == q[j]) dup[j] = 1;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (u64 t = 1; t < nt; ++t) th.emplace_back(work, m * t / nt, m * (t + 1) / nt);
+  work(0, m / nt);
+  for (auto& t : th) t.join();
+}
+
+// Drop from the level being built, [d, d + n_new) in the device window, the
+// states the host runs already hold (stable: TLC order survives).  Returns
+// the new count, or ~0 on error.
+u64 tier_filter_level(tlcg_ctx* c, u64 d, u64 n_new) {
+  if (c->runs.empty() || !n_new) return n_new;
+  if (n_new > c->filt_cap) {
+    hipFree(c->d_q); hipFree(c->d_keep); hipFree(c->d_sel); hipFree(c->d_ftmp); hipFree(c->d_qn);
+    c->d_q = c->d_sel = nullptr;
+    c->d_keep = nullptr;
+    c->d_ftmp = nullptr;
+    c->d_qn = nullptr;
+    c->filt_cap = 0;
+    const u64 cap = std::max<u64>(n_new + n_new / 4, 1u << 16);
+    size_t t1 = 0, t2 = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (const u64*)nullptr, (u64*)nullptr, (const u64*)nullptr,
+                                           (u64*)nullptr, (int)cap, 0, 64, c->stream) != hipSuccess ||
+        hipcub::DeviceSelect::Flagged(nullptr, t2, (const u64*)nullptr, (const unsigned char*)nullptr, (u64*)nullptr,
+                                      (unsigned long long*)nullptr, (int)cap, c->stream) != hipSuccess)
+      return ~0ull;
+    c->ftmp_bytes = std::max(t1, t2);
+    if (!alloc_bytes(c, (void**)&c->d_q, cap * 8 * 4, "FPSet tier queue") ||
+        !alloc_bytes(c, (void**)&c->d_keep, cap, "FPSet tier flags") ||
+        !alloc_bytes(c, (void**)&c->d_sel, cap * 8, "FPSet tier select") ||
+        !alloc_bytes(c, &c->d_ftmp, c->ftmp_bytes, "FPSet tier scratch") ||
+        !alloc_bytes(c, (void**)&c->d_qn, 16, "FPSet tier counter"))
+      return ~0ull;
+    c->filt_cap = cap;
+  }
+  const u64 cap = c->filt_cap;
+  u64 *q_key = c->d_q, *q_pos = c->d_q + cap, *q_key2 = c->d_q + 2 * cap, *q_pos2 = c->d_q + 3 * cap;
+  u64* lvl = dev_state(c, d);
+  double t0 = wall_ms();
+  HIPCHK_U(hipMemsetAsync(c->d_qn, 0, 16, c->stream));
+  k_tier_filter<<<grid_for(n_new, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(lvl, n_new, c->d_bloom, c->bloom_log2,
+                                                                              q_key, q_pos, c->d_qn);
+  HIPCHK_U(hipGetLastError());
+  unsigned long long m = 0;
+  HIPCHK_U(hipMemcpyAsync(&m, c->d_qn, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK_U(hipStreamSynchronize(c->stream));
+  c->tier_queued += m;
+  c->tier_ms[1] += wall_ms() - t0;
+  t0 = wall_ms();
+  if (!m) return n_new;
+  // sorted queries walk the runs in order
+  size_t tmp = c->ftmp_bytes;
+  HIPCHK_U(hipcub::DeviceRadixSort::SortPairs(c->d_ftmp, tmp, q_key, q_key2, q_pos, q_pos2, (int)m, 0, 64, c->stream));
+  std::vector<u64> hq(m);
+  std::vector<unsigned char> dup(m);
+  HIPCHK_U(hipMemcpyAsync(hq.data(), q_key2, m * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK_U(hipStreamSynchronize(c->stream));
+  host_tier_lookup(c, hq.data(), m, dup.data());
+  u64 ndup = 0;
+  for (u64 j = 0; j < m; ++j) ndup += dup[j];
+  c->tier_dups += ndup;
+  c->tier_ms[2] += wall_ms() - t0;
+  t0 = wall_ms();
+  if (!ndup) return n_new;
+  unsigned char* d_dup = (unsigned char*)q_key;  // the unsorted keys are no longer needed
+  HIPCHK_U(hipMemcpyAsync(d_dup, dup.data(), m, hipMemcpyHostToDevice, c->stream));
+  HIPCHK_U(hipMemsetAsync(c->d_keep, 1, n_new, c->stream));
+  k_tier_mark<<<grid_for(m, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(q_pos2, d_dup, m, c->d_keep);
+  HIPCHK_U(hipGetLastError());
+  // compact states and parent refs in place, keeping their order
+  unsigned long long kept = 0;
+  u64* arrays[2] = {lvl, dev_parent(c, d)};
+  for (u64* arr : arrays) {
+    tmp = c->ftmp_bytes;
+    HIPCHK_U(hipcub::DeviceSelect::Flagged(c->d_ftmp, tmp, arr, c->d_keep, c->d_sel, c->d_qn, (int)n_new, c->stream));
+    HIPCHK_U(hipMemcpyAsync(arr, c->d_sel, n_new * 8, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIPCHK_U(hipMemcpyAsync(&kept, c->d_qn, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK_U(hipStreamSynchronize(c->stream));
+  c->tier_ms[3] += wall_ms() - t0;
+  if (kept != n_new - ndup) {
+    c->err = "internal: FPSet tier compaction count";
+    return ~0ull;
+  }
+  return kept;
+}
+
+// The host tier's flush point: a level boundary, keeping the newest levels
+// (up to 4) in the HBM table when the table still fits `need` (a global index
+// end) under its cap -- most rediscovered states are a few levels old, and
+// those then never reach the host lookup.
+u64 tier_flush_point(tlcg_ctx* c, u64 need, int max_log2) {
+  const u64 d = distinct_of(c);
+  const size_t nl = c->level_base.size();
+  for (int keep = 4; keep > 0; --keep) {
+    if ((size_t)keep >= nl) continue;
+    const u64 g = c->level_base[nl - 1 - (size_t)keep];
+    if (g > c->t0_base && g < d && 2 * (need - g) <= (1ull << max_log2)) return g;
+  }
+  return d;
+}
+
+// keep the HBM table's load <= 1/2 for `need` states (a global index end):
+// grow it, or with the host tier move its older states to the host first
 bool ensure_fpset(tlcg_ctx* c, u64 need) {
-  int l = std::max(c->log2, 16);
-  while ((1ull << l) < 2 * need && l < 40) ++l;
+  auto size_for = [&](u64 n0) {
+    int l = std::max(c->log2, c->opts.fpset_spill ? 10 : 16);
+    while ((1ull << l) < 2 * n0 && l < 40) ++l;
+    return l;
+  };
+  int l = size_for(need - c->t0_base);
   if (c->d_slots && l == c->log2) return true;
+  const int mx = c->opts.fpset_spill ? fpset_max_log2(c) : 40;
+  if (c->opts.fpset_spill && l > mx && distinct_of(c) > c->t0_base) {
+    if (!flush_tier(c, tier_flush_point(c, need, mx))) return false;
+    l = size_for(need - c->t0_base);
+  }
   return rebuild_fpset(c, l, distinct_of(c) + c->pending);
+}
+
+// after an FPSet overflow: grow the table, or flush it to the host tier
+bool regrow_fpset(tlcg_ctx* c, unsigned ovf, u64 n) {
+  if (!(ovf & OVF_FPSET)) return rebuild_fpset(c, c->log2, n);
+  const u64 d = distinct_of(c);
+  const int mx = c->opts.fpset_spill ? fpset_max_log2(c) : 40;
+  if (c->opts.fpset_spill && c->log2 + 1 > mx && d > c->t0_base) {
+    if (!flush_tier(c, d)) return false;
+    return rebuild_fpset(c, c->log2, n);
+  }
+  return rebuild_fpset(c, c->log2 + 1, n);
 }
 
 bool ensure_scratch(tlcg_ctx* c, u64 n) {
@@ -867,6 +1299,14 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   st->engine = (uint64_t)c->engine;
   st->jit_used = c->jit_used ? 1 : 0;
   st->host_states = c->win;
+  st->fpset_host_states = c->t0_base;
+  if (std::getenv("TLCG_TIER_TRACE") && c->opts.fpset_spill)
+    std::fprintf(stderr,
+                 "tier: host states %llu in %zu runs, queued %llu, dups %llu, table 2^%d; ms flush %.1f "
+                 "filter %.1f lookup %.1f compact %.1f\n",
+                 (unsigned long long)c->t0_base, c->runs.size(), (unsigned long long)c->tier_queued,
+                 (unsigned long long)c->tier_dups, c->log2, c->tier_ms[0], c->tier_ms[1], c->tier_ms[2],
+                 c->tier_ms[3]);
   st->status = c->status;
   st->invariant = -1;
   st->action = -1;
@@ -881,13 +1321,6 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   st->kernel_ms = c->kernel_ms;
   st->expand_ms = c->expand_ms;
   st->levels_redone = c->levels_redone;
-}
-
-// the host chunk holding spilled state g (< win)
-const tlcg_ctx::HostChunk& chunk_of(const tlcg_ctx* c, u64 g) {
-  auto it = std::upper_bound(c->hchunks.begin(), c->hchunks.end(), g,
-                             [](u64 x, const tlcg_ctx::HostChunk& h) { return x < h.g0; });
-  return *(it - 1);
 }
 
 bool state_at(tlcg_ctx* c, u64 g, u128* s, u64* p) {
@@ -1169,7 +1602,7 @@ bool run_init(tlcg_ctx* c) {
   expect = std::min(expect, hm.n_init);
   if (!ensure_store(c, expect)) return false;
   if (!c->d_slots) {
-    int l = c->opts.log2_fpset_slots > 0 ? c->opts.log2_fpset_slots : 16;
+    int l = c->opts.log2_fpset_slots > 0 ? c->opts.log2_fpset_slots : c->opts.fpset_spill ? 10 : 16;
     while ((1ull << l) < 2 * expect && c->opts.log2_fpset_slots <= 0 && l < 40) ++l;
     if (!rebuild_fpset(c, l, 0)) return false;
   } else {
@@ -1342,7 +1775,7 @@ bool step_level(tlcg_ctx* c) {
   const u64 worst = F * (u64)hm.max_new_per_state;
   const u64 est = next_level_estimate(c, F);
   if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return false;
-  if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + est)) return false;
+  if ((c->opts.log2_fpset_slots <= 0 || c->opts.fpset_spill) && !ensure_fpset(c, d + est)) return false;
   if (!ensure_scratch(c, std::min(worst, dev_room(c, d)))) return false;
   for (;;) {
     if (!reset_ctr(c)) return false;
@@ -1373,9 +1806,10 @@ bool step_level(tlcg_ctx* c) {
       if (!ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * dev_room(c, d)))) return false;
       if (!ensure_scratch(c, dev_room(c, d))) return false;
     }
-    if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d)) return false;
+    if (!regrow_fpset(c, ovf, d)) return false;
   }
-  const u64 n_new = c->h_ctr->n_new;
+  u64 n_new = c->h_ctr->n_new;
+  if (c->opts.fpset_spill && (n_new = tier_filter_level(c, d, n_new)) == ~0ull) return false;
   c->generated += c->h_ctr->generated;
   if (n_new) c->level_base.push_back(d + n_new);
   if (c->h_ctr->event != NO_EVENT) return resolve_event(c, c->h_ctr->event, depth);
@@ -1421,6 +1855,11 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
     *out = c;
     return -2;
   }
+  if (c->opts.fpset_spill && c->words != 1) {
+    c->err = "the host FPSet tier keeps <= 63-bit states";
+    *out = c;
+    return -2;
+  }
   if (c->opts.engine == TLCG_ENGINE_COMPONENT && !component_applicable(c)) {
     c->err = "the component engine needs an immutable `messages` (no Producer), no TLC-order mode and a closed partition";
     *out = c;
@@ -1461,7 +1900,14 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_dkey_slot);
   hipFree(c->d_states);
   hipFree(c->d_parents);
+  free_tier(c);
   destroy_host_pool(c);
+  hipFree(c->d_bloom);
+  hipFree(c->d_q);
+  hipFree(c->d_keep);
+  hipFree(c->d_sel);
+  hipFree(c->d_ftmp);
+  hipFree(c->d_qn);
   hipFree(c->d_slot_new);
   hipFree(c->d_dk);
   hipFree(c->d_dk2);
@@ -1491,6 +1937,7 @@ void* tlcg_stream(tlcg_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
   if (!c || !c->stream) return -1;
+  free_tier(c);
   free_host_chunks(c);
   c->kernel_ms = c->expand_ms = 0;
   c->status = TLCG_RUNNING;
@@ -1859,8 +2306,16 @@ int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
   c->ev_parent_ref = NO_PARENT;
   c->ev_action = -1;
   // the FPSet is a function of the stored states: rebuild it from them
+  free_tier(c);
   int l = c->opts.log2_fpset_slots > 0 ? c->opts.log2_fpset_slots : std::max(c->log2, 16);
   while (c->opts.log2_fpset_slots <= 0 && (1ull << l) < 2 * d && l < 40) ++l;
+  if (c->opts.fpset_spill && l > fpset_max_log2(c)) {
+    // the host tier takes the committed states, half a table at a time
+    if (!rebuild_fpset(c, fpset_max_log2(c), 0)) return -10;
+    while (c->t0_base < d)
+      if (!flush_tier(c, std::min<u64>(d, c->t0_base + (1ull << c->log2) / 2))) return -10;
+    l = c->log2;
+  }
   if (!rebuild_fpset(c, l, d)) return -10;
   c->inited = true;
   fill_stats(c, st);
@@ -1902,7 +2357,7 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
   const u64 worst = F * (u64)hm.max_new_per_state;
   c->pending = 0;
   if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return -10;
-  if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + est)) return -10;
+  if ((c->opts.log2_fpset_slots <= 0 || c->opts.fpset_spill) && !ensure_fpset(c, d + est)) return -10;
   // outbox: an even split of the expected successors, with slack; grows on overflow
   u64 per_dst = F ? 2 * est / (u64)c->opts.world + 1024 : 1024;
   for (;;) {
@@ -1936,7 +2391,7 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
       per_dst = std::max<u64>(2 * per_dst, mx + mx / 4);
     }
     if ((ovf & OVF_STORE) && !ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * dev_room(c, d)))) return -10;
-    if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d)) return -10;
+    if (!regrow_fpset(c, ovf, d)) return -10;
   }
   c->generated += c->h_ctr->generated;
   c->pending = c->h_ctr->n_new;
@@ -1976,7 +2431,8 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
   const LevelCtr before = *c->h_ctr;      // the level's counters after the expand
   c->pending = local_new;
   if (!ensure_store(c, d + local_new + n_records)) return -10;
-  if (c->opts.log2_fpset_slots <= 0 && !ensure_fpset(c, d + local_new + n_records)) return -10;
+  if ((c->opts.log2_fpset_slots <= 0 || c->opts.fpset_spill) && !ensure_fpset(c, d + local_new + n_records))
+    return -10;
   for (;;) {
     if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
     k_absorb<<<grid_for(n_records, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
@@ -1993,7 +2449,7 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
     // grow and redo: forget this absorb's appends and inserts
     ++c->levels_redone;
     if ((ovf & OVF_STORE) && !ensure_store(c, d + local_new + n_records)) return -10;
-    if (!rebuild_fpset(c, c->log2 + ((ovf & OVF_FPSET) ? 1 : 0), d + local_new)) return -10;
+    if (!regrow_fpset(c, ovf, d + local_new)) return -10;
     *c->h_ctr = before;
     if (hipMemcpyAsync(c->d_ctr, c->h_ctr, sizeof(LevelCtr), hipMemcpyHostToDevice, c->stream) != hipSuccess)
       return -10;
@@ -2049,8 +2505,9 @@ int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st) {
   if (!c) return -1;
   if (c->status == TLCG_RUNNING) {
     const int depth = (int)c->level_base.size() - 1;
-    const u64 n_new = c->h_ctr->n_new;
     const u64 d = distinct_of(c);
+    u64 n_new = c->h_ctr->n_new;
+    if (c->opts.fpset_spill && (n_new = tier_filter_level(c, d, n_new)) == ~0ull) return -10;
     c->level_base.push_back(d + n_new);  // empty levels kept (see run_init)
     c->pending = 0;
     if (c->h_ctr->event != NO_EVENT) {

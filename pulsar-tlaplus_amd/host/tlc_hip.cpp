@@ -196,6 +196,7 @@ int main(int argc, char** argv) {
   // like TLC's disk-backed trace and queue: committed levels move to host
   // memory when HBM runs short (never otherwise)
   opts.spill = 1;
+  opts.fpset_spill = tlcg_state_words(&model) == 1;  // and TLC's DiskFPSet: the host tier (narrow states)
   if (!recover_file.empty()) opts.engine = TLCG_ENGINE_GLOBAL;  // checkpoints are global-engine level states
   else std::printf("Computing initial states...\n");
   tlcg_ctx* ctx = nullptr;

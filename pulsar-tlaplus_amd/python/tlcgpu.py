@@ -44,7 +44,7 @@ class tlcg_opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("log2_fpset_slots", C.c_int32), ("state_capacity", C.c_uint64),
                 ("tlc_order", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32), ("partition", C.c_int32),
                 ("engine", C.c_int32), ("spill", C.c_int32), ("device_store_cap", C.c_uint64),
-                ("reserved", C.c_int32 * 4)]
+                ("fpset_spill", C.c_int32), ("log2_fpset_max", C.c_int32), ("reserved", C.c_int32 * 2)]
 
 
 class tlcg_stats(C.Structure):
@@ -52,7 +52,7 @@ class tlcg_stats(C.Structure):
                 ("depth", C.c_int32), ("status", C.c_int32), ("invariant", C.c_int32), ("action", C.c_int32),
                 ("event_gidx", C.c_uint64), ("fp_collision_optimistic", C.c_double), ("kernel_ms", C.c_double),
                 ("expand_ms", C.c_double), ("levels_redone", C.c_uint64), ("engine", C.c_uint64),
-                ("jit_used", C.c_uint64), ("host_states", C.c_uint64), ("reserved", C.c_uint64 * 1)]
+                ("jit_used", C.c_uint64), ("host_states", C.c_uint64), ("fpset_host_states", C.c_uint64)]
 
 
 _lib = None
@@ -266,6 +266,7 @@ class Result:
     levels_redone: int = 0
     engine: str = ""
     host_states: int = 0
+    fpset_host_states: int = 0
     trace: List[Tuple[str, int]] = field(default_factory=list)
 
 
@@ -274,7 +275,8 @@ class Checker:
 
     def __init__(self, model: Model, device: int = 0, log2_fpset_slots: int = 0, state_capacity: int = 0,
                  tlc_order: bool = False, rank: int = 0, world: int = 1, partition: int = 0,
-                 engine: str = "auto", spill: bool = False, device_store_cap: int = 0):
+                 engine: str = "auto", spill: bool = False, device_store_cap: int = 0,
+                 fpset_spill: bool = False, log2_fpset_max: int = 0):
         self.lib = load_library()
         self.model = model
         self._m = model.to_c()
@@ -283,6 +285,7 @@ class Checker:
         o.tlc_order, o.rank, o.world, o.partition = int(tlc_order), rank, world, partition
         o.engine = ENGINES[engine]
         o.spill, o.device_store_cap = int(spill), device_store_cap
+        o.fpset_spill, o.log2_fpset_max = int(fpset_spill), log2_fpset_max
         self._o = o
         self.ctx = C.c_void_p()
         rc = self.lib.tlcg_create(C.byref(self._m), C.byref(o), C.byref(self.ctx))
@@ -362,7 +365,8 @@ class Checker:
                    left_on_queue=0 if status == "ok" else s.frontier, levels=self.level_sizes(),
                    collision_optimistic=s.fp_collision_optimistic, kernel_ms=s.kernel_ms,
                    expand_ms=s.expand_ms, levels_redone=s.levels_redone,
-                   engine={v: k for k, v in ENGINES.items()}.get(s.engine, "?"), host_states=s.host_states)
+                   engine={v: k for k, v in ENGINES.items()}.get(s.engine, "?"), host_states=s.host_states,
+                   fpset_host_states=s.fpset_host_states)
         if s.invariant >= 0:
             r.invariant = self.model.invariants[s.invariant]
         if s.action >= 0:
