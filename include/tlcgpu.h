@@ -215,6 +215,11 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
  * order; the counterexample is that state followed by stuttering), -1 when
  * the property holds, < -1 on a bad model. */
 int64_t tlcg_host_termination_counterexample(const tlcg_model* m);
+/* Enable xGMI peer access among devices 0..n-1 (one process driving contexts
+ * on several devices, e.g. tlc-hip -gpus N).  Returns the pairs enabled. */
+int tlcg_peer_access(int32_t n);
+/* HIP devices visible to this process (0 without a GPU). */
+int tlcg_device_count(void);
 /* Owner rank of a state under the context's partition. */
 int tlcg_owner(tlcg_ctx* c, uint64_t state);
 
@@ -236,6 +241,25 @@ int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n);
  * buffer; sum of the tlcg_outbox counts x 16 bytes), one stream sync. */
 int tlcg_outbox_gather(tlcg_ctx* c, void* out);
 int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats* st);
+/* The exchange when one process drives every rank (ctxs[r] = rank r of n, on
+ * devices with peer access, tlcg_peer_access): after tlcg_expand on all of
+ * them, copies each outbox into its owner's inbox device-to-device (source-
+ * rank-major, as an all-to-all delivers) and waits for the copies.  n_in[d] =
+ * records for tlcg_absorb(ctxs[d], n_in[d], ...).  Replaces distributed
+ * TLC's FPSetManager.putBlock round trips within one node. */
+int tlcg_exchange_local(tlcg_ctx* const* ctxs, int32_t n, uint64_t* n_in);
+/* 1 when no successor leaves its rank (partition by an immutable `messages`):
+ * each rank then runs tlcg_run alone and only the counts are combined. */
+int tlcg_partition_closed(const tlcg_ctx* c);
+/* The whole check by one process on the node's GPUs (tlc-hip -gpus N): n
+ * ranks, rank r on device r mod tlcg_device_count(), each driven from its own
+ * host thread; a closed partition runs each rank to completion, an open one
+ * runs expand -> tlcg_exchange_local -> absorb per level.  *st gets the
+ * combined verdict (counts summed, the lowest failing rank's error, depth from
+ * the summed level sizes, which go to levels[0..cap) and *n_levels).  The
+ * contexts are destroyed before return; a trace is re-derived on one GPU. */
+int tlcg_run_node(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_stats* st, uint64_t* levels,
+                  int32_t cap, int32_t* n_levels, char* err, int32_t err_cap);
 
 /* TLC -checkpoint: write the run's committed levels (state store + parent
  * log, level sizes, counters) to `path` between levels of a global-engine

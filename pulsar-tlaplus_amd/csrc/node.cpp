@@ -1,0 +1,146 @@
+// pulsar-tlaplus_amd/csrc/node.cpp -- tlcg_run_node: one process checks the
+// model on every GPU of a node, one context (rank) per device, the FPSet
+// hash-partitioned by owner.  This is the single-process form of TLC's
+// distributed FPSetManager (tlc2.tool.fp) that `tlc-hip -gpus N` runs; the
+// one-process-per-GPU form over RCCL is python/dist.py.  It uses only the
+// C-ABI of include/tlcgpu.h: every call makes its context's device current,
+// so each rank is driven from its own host thread.
+//
+//   closed partition (no Producer: `messages` is immutable, so successors never
+//     leave their rank, compaction.tla:87,100,132,139,145,151,165,182,186,214):
+//     every rank runs tlcg_run to completion, then the counts are combined;
+//   open partition (Producer, or tlcg_opts.partition = 2): every level is
+//     tlcg_expand on all ranks -> tlcg_exchange_local (device-to-device copies
+//     of the {state, parent} records to their owners over xGMI) ->
+//     tlcg_absorb + tlcg_end_level, until a rank stops or no rank found a new
+//     state.
+#include <algorithm>
+#include <cstdio>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tlcgpu.h"
+
+namespace {
+
+// f(r) for every rank on its own host thread; the first nonzero result (or 0)
+template <class F>
+int on_all(int n, F f) {
+  std::vector<int> rc((size_t)n, 0);
+  std::vector<std::thread> th;
+  for (int r = 0; r < n; ++r) th.emplace_back([&, r] { rc[(size_t)r] = f(r); });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < n; ++r)
+    if (rc[(size_t)r]) return rc[(size_t)r];
+  return 0;
+}
+
+void put_err(char* err, int32_t cap, const std::string& s) {
+  if (err && cap > 0) std::snprintf(err, (size_t)cap, "%s", s.c_str());
+}
+
+}  // namespace
+
+extern "C" int tlcg_run_node(const tlcg_model* m, const tlcg_opts* base, int32_t n, tlcg_stats* st,
+                             uint64_t* levels_out, int32_t cap, int32_t* n_levels, char* err, int32_t err_cap) {
+  if (!m || !base || !st || n < 1 || n > 64) {
+    put_err(err, err_cap, "tlcg_run_node: bad arguments");
+    return -1;
+  }
+  const int ndev = std::max(1, tlcg_device_count());
+  std::vector<tlcg_ctx*> ctxs((size_t)n, nullptr);
+  std::vector<tlcg_stats> sts((size_t)n);
+  auto fail = [&](int r, const char* what, int code) {
+    put_err(err, err_cap, std::string(what) + " (rank " + std::to_string(r) + "): " +
+                              (ctxs[(size_t)r] ? tlcg_last_error(ctxs[(size_t)r]) : "no context"));
+    for (auto* c : ctxs) tlcg_destroy(c);
+    return code < 0 ? code : -1;
+  };
+  // the first rank whose call failed (its context holds the message)
+  auto first_bad = [&](const std::vector<int>& rc) {
+    for (int r = 0; r < n; ++r)
+      if (rc[(size_t)r]) return r;
+    return 0;
+  };
+  std::vector<int> rc((size_t)n, 0);
+  auto all = [&](auto f) {
+    return on_all(n, [&](int r) { return rc[(size_t)r] = f(r); });
+  };
+  tlcg_peer_access(std::min(n, ndev));
+  for (int r = 0; r < n; ++r) {
+    tlcg_opts o = *base;
+    o.device = r % ndev;  // more ranks than devices: ranks share a device
+    o.rank = r;
+    o.world = n;
+    const int c = tlcg_create(m, &o, &ctxs[(size_t)r]);
+    if (c) return fail(r, "tlcg_create", c);
+  }
+  if (tlcg_partition_closed(ctxs[0]) == 1) {
+    if (int c = all([&](int r) { return tlcg_run(ctxs[(size_t)r], &sts[(size_t)r]); })) return fail(first_bad(rc), "tlcg_run", c);
+  } else {
+    if (int c = all([&](int r) { return tlcg_init(ctxs[(size_t)r], &sts[(size_t)r]); })) return fail(first_bad(rc), "tlcg_init", c);
+    std::vector<uint64_t> n_in((size_t)n, 0);
+    for (;;) {
+      bool any_new = false, any_stop = false;
+      for (const auto& s : sts) {
+        any_new |= s.frontier > 0;
+        any_stop |= s.status != TLCG_RUNNING;
+      }
+      if (any_stop || !any_new) break;
+      if (int c = all([&](int r) { return tlcg_expand(ctxs[(size_t)r], &sts[(size_t)r]); }))
+        return fail(first_bad(rc), "tlcg_expand", c);
+      if (int c = tlcg_exchange_local(ctxs.data(), n, n_in.data())) return fail(0, "tlcg_exchange_local", c);
+      if (int c = all([&](int r) {
+            const int a = tlcg_absorb(ctxs[(size_t)r], n_in[(size_t)r], &sts[(size_t)r]);
+            return a ? a : tlcg_end_level(ctxs[(size_t)r], &sts[(size_t)r]);
+          }))
+        return fail(first_bad(rc), "tlcg_absorb/tlcg_end_level", c);
+    }
+  }
+  // combine: counts sum, device times max, the first error's verdict and depth
+  tlcg_stats out = sts[0];
+  out.generated = out.distinct = out.frontier = out.levels_redone = out.host_states = out.fpset_host_states = 0;
+  out.kernel_ms = out.expand_ms = 0;
+  int first = -1;
+  for (int r = 0; r < n; ++r) {
+    const tlcg_stats& s = sts[(size_t)r];
+    out.generated += s.generated;
+    out.distinct += s.distinct;
+    out.frontier += s.frontier;
+    out.levels_redone += s.levels_redone;
+    out.host_states += s.host_states;
+    out.fpset_host_states += s.fpset_host_states;
+    out.kernel_ms = std::max(out.kernel_ms, s.kernel_ms);
+    out.expand_ms = std::max(out.expand_ms, s.expand_ms);
+    // the first error is the one in the lowest level (a closed partition's
+    // ranks run on independently past another rank's error), then lowest rank
+    if (s.status != TLCG_DONE && s.status != TLCG_RUNNING && (first < 0 || s.depth < sts[(size_t)first].depth))
+      first = r;
+  }
+  out.status = first < 0 ? TLCG_DONE : sts[(size_t)first].status;
+  out.invariant = first < 0 ? -1 : sts[(size_t)first].invariant;
+  out.action = first < 0 ? -1 : sts[(size_t)first].action;
+  out.event_gidx = first < 0 ? ~0ull : sts[(size_t)first].event_gidx;
+  // per-level sizes summed over ranks (partitioned ranks keep empty levels,
+  // so trailing empty ones are dropped); depth = their number
+  std::vector<uint64_t> levels, mine(1 << 12);
+  for (int r = 0; r < n; ++r) {
+    int32_t k = 0;
+    if (tlcg_level_sizes(ctxs[(size_t)r], mine.data(), (int32_t)mine.size(), &k) != 0)
+      return fail(r, "tlcg_level_sizes", -1);
+    k = std::min<int32_t>(k, (int32_t)mine.size());
+    if ((size_t)k > levels.size()) levels.resize((size_t)k, 0);
+    for (int32_t i = 0; i < k; ++i) levels[(size_t)i] += mine[(size_t)i];
+  }
+  while (!levels.empty() && !levels.back()) levels.pop_back();
+  out.depth = first < 0 ? (int32_t)levels.size() : sts[(size_t)first].depth;
+  const double d = (double)out.distinct, g = (double)out.generated;
+  out.fp_collision_optimistic = d * (g - d) / 18446744073709551616.0;
+  if (levels_out)
+    for (size_t i = 0; i < levels.size() && (int32_t)i < cap; ++i) levels_out[i] = levels[i];
+  if (n_levels) *n_levels = (int32_t)levels.size();
+  for (auto* c : ctxs) tlcg_destroy(c);
+  *st = out;
+  return 0;
+}

@@ -673,7 +673,24 @@ namespace {
     }                                                                             \
   } while (0)
 
+// Every entry point that allocates, copies or launches makes the context's
+// device current for its call: contexts of several devices can then be
+// driven from any host thread (tlc-hip -gpus N runs one thread per device).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(const tlcg_ctx* c);
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 u64 distinct_of(const tlcg_ctx* c) { return c->level_base.empty() ? 0 : c->level_base.back(); }
+DeviceGuard::DeviceGuard(const tlcg_ctx* c) {
+  int cur = -1;
+  if (c && hipGetDevice(&cur) == hipSuccess && cur != c->opts.device && hipSetDevice(c->opts.device) == hipSuccess)
+    prev = cur;
+}
+
 // device address of the state / parent ref with global index g (g >= win)
 u64* dev_state(tlcg_ctx* c, u64 g) { return c->d_states + (g - c->win) * c->words; }
 u64* dev_parent(tlcg_ctx* c, u64 g) { return c->d_parents + (g - c->win); }
@@ -1578,7 +1595,16 @@ int run_component(tlcg_ctx* c) {
   }
   if (n) return 0;  // components beyond 255 states / 48 levels: the global engine takes the model
   while (!c->comp_levels.empty() && c->comp_levels.back() == 0) c->comp_levels.pop_back();
-  if (best_ev != NO_EVENT) return resolve_comp_event(c, best_ev) ? 1 : -1;
+  if (best_ev != NO_EVENT) {
+    if (!resolve_comp_event(c, best_ev)) return -1;
+    // like the level loop, stop at the end of the level that found the error:
+    // depth and distinct count to there (every lane ran its component out)
+    const size_t lv = (size_t)(best_ev >> 56) + 1;
+    if (c->comp_levels.size() > lv) c->comp_levels.resize(lv);
+    c->comp_distinct = 0;
+    for (u64 x : c->comp_levels) c->comp_distinct += x;
+    return 1;
+  }
   c->status = TLCG_DONE;
   return 1;
 }
@@ -1895,6 +1921,7 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
 
 void tlcg_destroy(tlcg_ctx* c) {
   if (!c) return;
+  const DeviceGuard dg(c);
   if (c->stream) hipStreamSynchronize(c->stream);
   hipFree(c->d_slots);
   hipFree(c->d_dkey_slot);
@@ -1936,6 +1963,7 @@ const char* tlcg_last_error(const tlcg_ctx* c) { return c ? c->err.c_str() : "nu
 void* tlcg_stream(tlcg_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
+  const DeviceGuard dg(c);
   if (!c || !c->stream) return -1;
   free_tier(c);
   free_host_chunks(c);
@@ -1966,6 +1994,7 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
 }
 
 int tlcg_step_level(tlcg_ctx* c, tlcg_stats* st) {
+  const DeviceGuard dg(c);
   if (!c || !c->inited) return -1;
   if (c->engine == TLCG_ENGINE_COMPONENT) {  // the run finished in tlcg_init
     fill_stats(c, st);
@@ -2006,6 +2035,7 @@ int tlcg_level_sizes(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
 }
 
 int tlcg_state_at_words(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref) {
+  const DeviceGuard dg(c);
   if (!c || gidx >= store_end(c)) return -1;
   u128 s = 0;
   u64 p = 0;
@@ -2024,6 +2054,7 @@ int tlcg_state_at(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_
 }
 
 int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
+  const DeviceGuard dg(c);
   if (!c || first + n > store_end(c)) return -1;
   const u64 w = c->words;
   while (n && first < c->win) {  // spilled states
@@ -2050,6 +2081,7 @@ int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
 }
 
 int tlcg_trace_words(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len) {
+  const DeviceGuard dg(c);
   if (!c) return -1;
   if (c->ev_word == NO_EVENT) {
     c->err = "no violation to trace";
@@ -2175,6 +2207,7 @@ bool file_to_dev(tlcg_ctx* c, FILE* f, void* dev, size_t bytes, void* stage) {
 extern "C" {
 
 int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
+  const DeviceGuard dg(c);
   if (!c || !path) return -1;
   if (!c->inited) {
     c->err = "nothing to checkpoint: call tlcg_init first";
@@ -2232,6 +2265,7 @@ int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
 }
 
 int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
+  const DeviceGuard dg(c);
   if (!c || !path) return -1;
   FILE* f = std::fopen(path, "rb");
   if (!f) {
@@ -2335,6 +2369,32 @@ int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t 
   return (int)code.size();
 }
 
+// Let devices 0..n-1 read and write each other's memory (xGMI peer access),
+// for contexts of one process on several devices that exchange records by
+// device-to-device copies.  Returns the number of pairs enabled.
+int tlcg_peer_access(int32_t n) {
+  int cur = 0, count = 0, pairs = 0;
+  if (hipGetDevice(&cur) != hipSuccess || hipGetDeviceCount(&count) != hipSuccess) return -1;
+  n = std::min(n, count);
+  for (int a = 0; a < n; ++a) {
+    if (hipSetDevice(a) != hipSuccess) continue;
+    for (int b = 0; b < n; ++b) {
+      int can = 0;
+      if (a == b || hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+      const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+      if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) ++pairs;
+      (void)hipGetLastError();
+    }
+  }
+  (void)hipSetDevice(cur);
+  return pairs;
+}
+
+int tlcg_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 int tlcg_owner(tlcg_ctx* c, uint64_t state) {
   if (!c) return -1;  // wide states: pass the low word (the partition key lies there)
   return (int)(((mix64(state & c->owner_mask) >> 32) * (u64)c->opts.world) >> 32);
@@ -2343,6 +2403,7 @@ int tlcg_owner(tlcg_ctx* c, uint64_t state) {
 // ---- partitioned levels (world > 1) ----
 
 int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
+  const DeviceGuard dg(c);
   if (!c || !c->inited) return -1;
   if (c->status != TLCG_RUNNING) {
     fill_stats(c, st);
@@ -2407,6 +2468,7 @@ int tlcg_outbox(tlcg_ctx* c, int32_t dst, void** dev_records, uint64_t* n_record
 }
 
 int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records) {
+  const DeviceGuard dg(c);
   if (!c) return -1;
   if (n_records > c->inbox_cap) {
     hipFree(c->d_inbox);
@@ -2421,6 +2483,7 @@ int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records) {
 }
 
 int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
+  const DeviceGuard dg(c);
   if (!c || n_records > c->inbox_cap) return -1;
   if (c->status != TLCG_RUNNING || !n_records) {
     fill_stats(c, st);
@@ -2462,6 +2525,7 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
 // Copy the first n records for `dst` to caller memory (host or device; the
 // runtime infers which), ordered after the expand on the context's stream.
 int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n) {
+  const DeviceGuard dg(c);
   if (!c || dst < 0 || dst >= c->opts.world || dst == c->opts.rank) return -1;
   if (!n) return 0;
   if (!c->d_outbox || n > c->h_ctr->n_out[dst] || n > c->outbox_cap) return -1;
@@ -2474,6 +2538,7 @@ int tlcg_outbox_read(tlcg_ctx* c, int32_t dst, void* out, uint64_t n) {
 // own, always empty, skipped), copied to one caller buffer with one stream
 // synchronization: the send buffer of an all-to-all.
 int tlcg_outbox_gather(tlcg_ctx* c, void* out) {
+  const DeviceGuard dg(c);
   if (!c) return -1;
   u64 off = 0;
   for (int dst = 0; dst < c->opts.world; ++dst) {
@@ -2492,6 +2557,7 @@ int tlcg_outbox_gather(tlcg_ctx* c, void* out) {
 // tlcg_inbox + copy + tlcg_absorb in one call: the copy of the caller's
 // records (host or device) and the insert run in order on the context's stream.
 int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats* st) {
+  const DeviceGuard dg(c);
   if (!c) return -1;
   if (n) {
     const int r = tlcg_inbox(c, n, nullptr);
@@ -2501,7 +2567,52 @@ int tlcg_absorb_records(tlcg_ctx* c, const void* records, uint64_t n, tlcg_stats
   return tlcg_absorb(c, n, st);
 }
 
+// The exchange of one process driving every rank (contexts on devices of one
+// node, peer access enabled): each destination's inbox receives the records
+// of every source, source-rank-major (the order an all-to-all delivers), by
+// device-to-device copies over xGMI on the source streams.  Returns with all
+// copies landed; n_in[d] = records now in ctxs[d]'s inbox, for tlcg_absorb.
+int tlcg_exchange_local(tlcg_ctx* const* ctxs, int32_t n, uint64_t* n_in) {
+  if (!ctxs || n < 1 || !n_in) return -1;
+  for (int r = 0; r < n; ++r)
+    if (!ctxs[r] || ctxs[r]->opts.world != n || ctxs[r]->opts.rank != r) return -1;
+  for (int dst = 0; dst < n; ++dst) {
+    tlcg_ctx* c = ctxs[dst];
+    u64 total = 0;
+    for (int src = 0; src < n; ++src)
+      if (src != dst) total += ctxs[src]->h_ctr->n_out[dst];
+    n_in[dst] = total;
+    if (!total) continue;
+    const int r = tlcg_inbox(c, total, nullptr);  // sized before any copy lands in it
+    if (r) return r;
+  }
+  for (int src = 0; src < n; ++src) {
+    tlcg_ctx* c = ctxs[src];
+    const DeviceGuard dg(c);
+    for (int dst = 0; dst < n; ++dst) {
+      if (dst == src) continue;
+      u64 at = 0;
+      for (int s = 0; s < src; ++s)
+        if (s != dst) at += ctxs[s]->h_ctr->n_out[dst];
+      const u64 k = c->h_ctr->n_out[dst];
+      if (!k) continue;
+      if (!c->d_outbox || k > c->outbox_cap) return -1;
+      HIPCHK_I(hipMemcpyPeerAsync(ctxs[dst]->d_inbox + 2 * at, ctxs[dst]->opts.device,
+                                  c->d_outbox + 2 * (u64)dst * c->outbox_cap, c->opts.device, k * 16, c->stream));
+    }
+  }
+  for (int src = 0; src < n; ++src) {
+    tlcg_ctx* c = ctxs[src];
+    const DeviceGuard dg(c);
+    HIPCHK_I(hipStreamSynchronize(c->stream));
+  }
+  return 0;
+}
+
+int tlcg_partition_closed(const tlcg_ctx* c) { return c ? (int)c->closed : -1; }
+
 int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st) {
+  const DeviceGuard dg(c);
   if (!c) return -1;
   if (c->status == TLCG_RUNNING) {
     const int depth = (int)c->level_base.size() - 1;

@@ -5,6 +5,7 @@
 // generated, distinct states, depth, verdict and (on an error) the trace.
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <cmath>
@@ -69,7 +70,7 @@ std::string prob_str(double p) {  // Java-like "3.8E-11"
 
 void usage() {
   std::fprintf(stderr,
-               "usage: tlc-hip [-config FILE.cfg] [-deadlock] [-workers N] [-gpu D] [-fpbits B]\n"
+               "usage: tlc-hip [-config FILE.cfg] [-deadlock] [-workers N] [-gpu D | -gpus N] [-fpbits B]\n"
                "               [-checkpoint MINUTES] [-metadir DIR] [-recover DIR]\n"
                "               [-tlc-order] [-no-trace] [-json] [-dump-defs] SPEC.tla\n");
 }
@@ -77,7 +78,7 @@ void usage() {
 struct Opts {
   std::string spec, cfg, metadir, recover;
   bool deadlock_off = false, tlc_order = false, trace = true, json = false, dump_defs = false;
-  int gpu = 0, fpbits = 0;
+  int gpu = 0, gpus = 1, fpbits = 0;
   double checkpoint_min = 30.0;  // TLC's default interval; 0 = never
 };
 
@@ -135,6 +136,7 @@ int main(int argc, char** argv) {
     }
     else if (a == "-cleanup" || a == "-nowarning" || a == "-terse") {}
     else if (a == "-gpu") o.gpu = std::atoi(next().c_str());
+    else if (a == "-gpus") o.gpus = std::atoi(next().c_str());
     else if (a == "-fpbits") o.fpbits = std::atoi(next().c_str());
     else if (a == "-tlc-order") o.tlc_order = true;
     else if (a == "-no-trace") o.trace = false;
@@ -145,6 +147,9 @@ int main(int argc, char** argv) {
     else o.spec = a;
   }
   if (o.spec.empty()) { usage(); return 255; }
+  if (o.gpus < 1 || o.gpus > 64) { std::fprintf(stderr, "Error: -gpus needs 1..64\n"); return 255; }
+  if (o.gpus > 1 && !o.recover.empty()) { std::fprintf(stderr, "Error: -recover runs on one GPU\n"); return 255; }
+  if (o.gpus > 1) o.checkpoint_min = 0;  // checkpoints hold one context's levels
   if (o.spec.size() < 4 || o.spec.substr(o.spec.size() - 4) != ".tla") o.spec += ".tla";
   if (o.cfg.empty()) o.cfg = o.spec.substr(0, o.spec.size() - 4) + ".cfg";
 
@@ -163,7 +168,11 @@ int main(int argc, char** argv) {
   auto t0 = std::chrono::steady_clock::now();
   std::printf("tlc-hip: TLC-compatible breadth-first model checking on MI355X (libtlcgpu ABI %d)\n",
               tlcg_abi_version());
-  std::printf("Running breadth-first search Model-Checking with 1 GPU (device %d) and seed 0.\n", o.gpu);
+  if (o.gpus > 1)
+    std::printf("Running breadth-first search Model-Checking with %d GPU ranks (FPSet partitioned by owner, rank r on device r mod %d) and seed 0.\n",
+                o.gpus, std::max(1, tlcg_device_count()));
+  else
+    std::printf("Running breadth-first search Model-Checking with 1 GPU (device %d) and seed 0.\n", o.gpu);
   std::printf("Parsing file %s\n", o.spec.c_str());
   if (!recognize_compaction(mod, &err)) { std::printf("Error: %s\n", err.c_str()); return 150; }
   if (!read_file(o.cfg, &cfgtext)) { std::printf("Error: cannot read configuration file %s\n", o.cfg.c_str()); return 150; }
@@ -200,13 +209,22 @@ int main(int argc, char** argv) {
   if (!recover_file.empty()) opts.engine = TLCG_ENGINE_GLOBAL;  // checkpoints are global-engine level states
   else std::printf("Computing initial states...\n");
   tlcg_ctx* ctx = nullptr;
-  if (tlcg_create(&model, &opts, &ctx) != 0) {
+  tlcg_stats st;
+  if (o.gpus > 1) {
+    char merr[512];
+    if (tlcg_run_node(&model, &opts, o.gpus, &st, nullptr, 0, nullptr, merr, sizeof merr) != 0) {
+      std::printf("Error: %s\n", merr);
+      return 255;
+    }
+    const unsigned long long n0 = (unsigned long long)tlcg_init_count(&model);
+    std::printf("Finished computing initial states: %llu distinct state%s generated at %s.\n", n0, n0 == 1 ? "" : "s",
+                now_str().c_str());
+  } else if (tlcg_create(&model, &opts, &ctx) != 0) {
     std::printf("Error: %s\n", ctx ? tlcg_last_error(ctx) : "tlcg_create failed");
     tlcg_destroy(ctx);
     return 255;
   }
-  tlcg_stats st;
-  if (!recover_file.empty()) {
+  if (ctx && !recover_file.empty()) {
     // [TLC-ext] TLC's recovery messages
     std::printf("Starting recovery from checkpoint %s\n", o.recover.c_str());
     if (tlcg_recover(ctx, recover_file.c_str(), &st) != 0) {
@@ -216,7 +234,7 @@ int main(int argc, char** argv) {
     }
     std::printf("Recovery completed. %llu states examined. %llu states on queue.\n",
                 (unsigned long long)(st.distinct - st.frontier), (unsigned long long)st.frontier);
-  } else {
+  } else if (ctx) {
     if (tlcg_init(ctx, &st) != 0) { std::printf("Error: %s\n", tlcg_last_error(ctx)); tlcg_destroy(ctx); return 255; }
     std::printf("Finished computing initial states: %llu distinct state%s generated at %s.\n",
                 (unsigned long long)st.distinct, st.distinct == 1 ? "" : "s", now_str().c_str());
@@ -275,9 +293,10 @@ int main(int argc, char** argv) {
     tlcg_ctx* tctx = ctx;
     tlcg_stats tst = st;
     bool own = false;
-    if (o.trace && !o.tlc_order) {
+    if (o.trace && (!o.tlc_order || !ctx)) {  // (after -gpus N: on one GPU)
       tlcg_opts to = opts;
       to.tlc_order = 1;
+      if (!ctx) to.device = 0;
       if (tlcg_create(&model, &to, &tctx) == 0 && tlcg_run(tctx, &tst) == 0 && tst.status == st.status) {
         own = true;
       } else {
@@ -306,7 +325,7 @@ int main(int argc, char** argv) {
         rc = 75;
         break;
     }
-    if (o.trace) {
+    if (o.trace && tctx) {
       const int words = tlcg_state_words(&model);  // 1, or 2 for a > 63-bit layout
       std::vector<uint64_t> states((size_t)words << 16);
       std::vector<int32_t> acts(1 << 16);

@@ -111,6 +111,11 @@ def load_library(path: str = LIB_PATH):
         "tlcg_copy_states_words": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
         "tlcg_absorb_records": (C.c_int, [P, P, U64, S]),
         "tlcg_stream": (P, [P]),
+        "tlcg_peer_access": (C.c_int, [I32]),
+        "tlcg_device_count": (C.c_int, []),
+        "tlcg_exchange_local": (C.c_int, [C.POINTER(P), I32, C.POINTER(U64)]),
+        "tlcg_partition_closed": (C.c_int, [P]),
+        "tlcg_run_node": (C.c_int, [M, O, I32, S, C.POINTER(U64), I32, C.POINTER(I32), C.c_char_p, I32]),
         "tlcg_jit_selftest": (C.c_int, [M, C.c_char_p, I32, C.c_char_p, I32][:1] + [C.c_char_p, C.c_char_p, I32]),
     }
     for name, (res, args) in sig.items():
@@ -387,3 +392,36 @@ def run(model: Model, **kw) -> Result:
         return ck.run()
     finally:
         ck.close()
+
+
+def run_node(model: Model, ranks: int, device: int = 0, log2_fpset_slots: int = 0, state_capacity: int = 0,
+             partition: int = 0, engine: str = "auto", spill: bool = False, device_store_cap: int = 0,
+             fpset_spill: bool = False, log2_fpset_max: int = 0) -> Result:
+    """The check by this one process on `ranks` contexts, rank r on device
+    r mod device_count (tlcg_run_node; `tlc-hip -gpus N`).  No trace: on an
+    error it is re-derived on one GPU (Checker(..., tlc_order=True))."""
+    lib = load_library()
+    m = model.to_c()
+    o = tlcg_opts()
+    o.device, o.log2_fpset_slots, o.state_capacity, o.partition = device, log2_fpset_slots, state_capacity, partition
+    o.engine = ENGINES[engine]
+    o.spill, o.device_store_cap = int(spill), device_store_cap
+    o.fpset_spill, o.log2_fpset_max = int(fpset_spill), log2_fpset_max
+    st = tlcg_stats()
+    lv = (C.c_uint64 * 65536)()
+    n = C.c_int32()
+    err = C.create_string_buffer(1024)
+    rc = lib.tlcg_run_node(C.byref(m), C.byref(o), ranks, C.byref(st), lv, 65536, C.byref(n), err, 1024)
+    if rc != 0:
+        raise RuntimeError(f"tlcg_run_node: {err.value.decode()} ({rc})")
+    status = STATUS[st.status]
+    r = Result(status=status, generated=st.generated, distinct=st.distinct, depth=st.depth,
+               left_on_queue=0 if status == "ok" else st.frontier, levels=[lv[i] for i in range(n.value)],
+               collision_optimistic=st.fp_collision_optimistic, kernel_ms=st.kernel_ms, expand_ms=st.expand_ms,
+               levels_redone=st.levels_redone, engine={v: k for k, v in ENGINES.items()}.get(st.engine, "?"),
+               host_states=st.host_states, fpset_host_states=st.fpset_host_states)
+    if st.invariant >= 0:
+        r.invariant = model.invariants[st.invariant]
+    if st.action >= 0:
+        r.action = ACTIONS[st.action]
+    return r

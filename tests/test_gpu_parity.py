@@ -25,6 +25,7 @@ def check_against_golden(case, r, tlc_order):
         return
     # an error stops the run at the end of the level that found it: the depth
     # and the trace are TLC's; generated/distinct are counted to that level end
+    assert r.depth == want["depth"], (case, r.engine, r.depth)
     m = model_of(GOLDEN[case]["constants"])
     want_trace = want["trace"]
     assert len(r.trace) == len(want_trace)

@@ -80,3 +80,33 @@ def test_m8_partitioned_matches_single():
     gen, distinct, levels, status = run_virtual(m, 4)
     assert (gen, distinct, status) == (147_039_563, 109_836_782, 1)
     assert len(levels) == 20
+
+
+# ---- tlcg_run_node: one process drives every rank (tlc-hip -gpus N) ----
+
+@pytest.mark.parametrize("ranks", [2, 3, 8])
+@pytest.mark.parametrize("case,partition", [("S", 0), ("S", 2), ("P_published", 0), ("X_producer_sparse", 0),
+                                            ("X_keys3_vals57", 2), ("W_C12", 0), ("D_N0_K1", 0)])
+def test_run_node_counts_invariant_in_ranks(case, partition, ranks):
+    want = GOLDEN[case]["result"]
+    r = tlcgpu.run_node(model_of(GOLDEN[case]["constants"]), ranks, partition=partition)
+    assert r.status == want["result"]
+    assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                             want["levels"])
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+@pytest.mark.parametrize("case,partition", [("V_leak", 0), ("V_dup", 0), ("V_leak_producer", 0), ("V_leak", 2)])
+def test_run_node_violation_verdict(case, partition, ranks):
+    want = GOLDEN[case]["result"]
+    r = tlcgpu.run_node(model_of(GOLDEN[case]["constants"]), ranks, partition=partition)
+    assert (r.status, r.invariant, r.depth) == (want["result"], want["invariant"], want["depth"])
+
+
+def test_run_node_matches_checker_engines():
+    # the closed partition runs either engine per rank; the open one the global engine
+    m = model_of(GOLDEN["S"]["constants"])
+    want = GOLDEN["S"]["result"]
+    for engine in ("auto", "global", "component"):
+        r = tlcgpu.run_node(m, 4, engine=engine)
+        assert (r.generated, r.distinct, r.levels) == (want["generated"], want["distinct"], want["levels"])
