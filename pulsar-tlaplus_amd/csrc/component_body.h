@@ -53,6 +53,11 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     u64* st = a.store + b * (u64)K * 64 + (u64)lane;
     u64* par = a.parents + b * (u64)K * 64 + (u64)lane;
     const u64 gbase = a.store_base + b * (u64)K * 64 + (u64)lane;
+    // wave-uniform bases + 32-bit lane offsets (saddr + voffset stores), and
+    // the parent reference of queue position 0 (+ pos << (6 + ord_bits) per position)
+    char* const stb = reinterpret_cast<char*>(a.store + b * (u64)K * 64);
+    char* const parb = reinterpret_cast<char*>(a.parents + b * (u64)K * 64);
+    const u64 pref = a.rank_tag | (gbase << L.ord_bits);
     int head = 0, tail = 0, level = 0, lvl_end = 0, lvl_start = 0;
     bool alive = act, ovf = false;
     u64 lgen = 0;
@@ -90,8 +95,9 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       h[sl][lane] = (uint8_t)(tail + 1);
       q[tail][lane] = key;
 #ifndef TLCG_NO_STORE  // (experiment only: measures what the HBM store costs)
-      st[(u64)tail * 64] = msgs | ((u64)key << mb);
-      par[(u64)tail * 64] = a.rank_tag | ((gbase + (u64)pos * 64) << L.ord_bits) | (u64)ordinal_of(L, action, 0);
+      const unsigned off = (unsigned)(tail * 64 + lane) * 8u;
+      *reinterpret_cast<u64*>(stb + off) = msgs | ((u64)key << mb);
+      *reinterpret_cast<u64*>(parb + off) = (pref + ((u64)pos << (6 + L.ord_bits))) | (u64)ordinal_of(L, action, 0);
 #endif
       ++tail;
       const int c = check_invariants_k(L, cmsg, key);
