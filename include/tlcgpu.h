@@ -184,6 +184,17 @@ int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out);
 int tlcg_trace_words(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len);
 int tlcg_state_at_words(tlcg_ctx* c, uint64_t gidx, uint64_t* state, uint64_t* parent_ref);
 int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out);
+/* TLC's "G states generated, D distinct states found, Q states left on
+ * queue." at the moment a one-worker TLC run stops on the error this context
+ * found (TLC prints it after the trace; replaces the end-of-level counts
+ * tlcg_stats carries at an error).  Follows ModelChecker.doNext: FIFO
+ * dequeue, Next disjuncts in order, each action's StateVec counted before its
+ * successors are inserted and checked, stop at the first violating new state,
+ * at a failing action (its successors uncounted) or after a deadlocked
+ * state's actions.  Needs a global-engine run in TLC order (tlcg_opts.tlc_order,
+ * world 1); refused after tlcg_recover.  [TLC-ext: restated from TLC's
+ * worker loop, not confirmable without TLC.] */
+int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, uint64_t* left_on_queue);
 /* Successor ordinal bits (to split a parent_ref). */
 int tlcg_ordinal_bits(const tlcg_model* m);
 int tlcg_action_of_ordinal(const tlcg_model* m, int32_t ordinal);

@@ -203,7 +203,8 @@ class Model:
             if k is not None:
                 b = bad(t)
                 if b:
-                    return dict(result=b[0], invariant=b[1], generated=generated, trace=trace(k))
+                    return dict(result=b[0], invariant=b[1], generated=generated, distinct=len(states),
+                                left_on_queue=len(states), trace=trace(k))
         levels.append(len(states))
         head = 0
         while head < len(states):
@@ -211,20 +212,40 @@ class Model:
             for p in range(head, end):
                 s = states[p]
                 n = 0
+
+                def stop(**kw):  # TLC's counters when the run stops while expanding p
+                    return dict(generated=generated, distinct=len(states), left_on_queue=len(states) - (p + 1), **kw)
+
+                def process(group):
+                    """one action's successors: counted as a whole (TLC's StateVec),
+                    then inserted and checked one by one"""
+                    nonlocal generated, n
+                    generated += len(group)
+                    n += len(group)
+                    for a, t in group:
+                        k = add(t, p, ACTIONS[a])
+                        if k is not None:
+                            b = bad(t)
+                            if b:
+                                return stop(result=b[0], invariant=b[1], trace=trace(k))
+                    return None
+
+                pending = []
                 try:
-                    succ = list(self.successors(s))
+                    for a, t in self.successors(s):
+                        if pending and pending[0][0] != a:
+                            r = process(pending)
+                            if r:
+                                return r
+                            pending = []
+                        pending.append((a, t))
                 except EvalError:
-                    return dict(result="action_error", generated=generated, trace=trace(p))
-                for a, t in succ:
-                    generated += 1
-                    n += 1
-                    k = add(t, p, ACTIONS[a])
-                    if k is not None:
-                        b = bad(t)
-                        if b:
-                            return dict(result=b[0], invariant=b[1], generated=generated, trace=trace(k))
+                    return stop(result="action_error", trace=trace(p))
+                r = process(pending)
+                if r:
+                    return r
                 if n == 0 and self.deadlock:
-                    return dict(result="deadlock", generated=generated, trace=trace(p))
+                    return stop(result="deadlock", trace=trace(p))
             head = end
             if len(states) > end:
                 levels.append(len(states) - end)

@@ -23,6 +23,13 @@
  *     every enabled Next disjunct, stuttering self-loops included;
  *   - invariants are checked, in cfg order, on every *new* state (inits too);
  *   - a state with no successor at all is a deadlock (unless -deadlock);
+ *   - at an error the run stops where TLC's worker stops
+ *     (ModelChecker.doNext): each action's successors are counted as a whole
+ *     before any is inserted and checked, so "generated" includes the rest of
+ *     the violating action's successors; a failing action's are not counted;
+ *     "distinct" includes the violating state, and "left_on_queue" is the
+ *     FIFO queue (distinct minus the states dequeued, the expanded one
+ *     included);
  *   - depth = number of BFS levels, the initial level counting as 1;
  *   - one worker: FIFO queue, Next disjuncts in source order
  *     (compaction.tla:216-231), first violation in generation order wins.
@@ -575,7 +582,7 @@ int main(int argc, char **argv) {
 
   uint64_t generated = 0;
   int result = R_OK, bad_inv = -1;
-  int64_t bad_parent = -1; int bad_action = -1; St bad_state; memset(&bad_state, 0, sizeof bad_state);
+  int64_t bad_parent = -1; int bad_action = -1; uint64_t dequeued = 0; St bad_state; memset(&bad_state, 0, sizeof bad_state);
   uint64_t level_start[4096]; int nlevels = 0;
   fp_grow();
 
@@ -619,6 +626,7 @@ int main(int argc, char **argv) {
     uint64_t lvl_end = n_states; /* current level [head, lvl_end) */
     for (; head < lvl_end && result == R_OK; head++) {
       St s; load_state(head, &s);
+      dequeued = head + 1;
       int nsucc = 0;
       /* Next, compaction.tla:216-231: disjuncts in source order */
       for (int a = 0; a < N_ACTIONS && result == R_OK; a++) {
@@ -637,8 +645,10 @@ int main(int argc, char **argv) {
           case A_TERMINATING: if (enabled_terminating(&s)) { out[0] = s; cnt = 1; } break;
         }
         if (rc == EV_ERROR) { result = R_ACTION_ERROR; bad_parent = (int64_t)head; bad_action = a; break; }
+        /* the action's successors are counted as a whole (TLC's StateVec,
+           ModelChecker.doNext) before any is inserted and checked */
+        generated += (uint64_t)cnt; nsucc += cnt;
         for (int j = 0; j < cnt && result == R_OK; j++) {
-          generated++; nsucc++;
           uint64_t k;
           if (fp_put(&out[j], (int64_t)head, a, &k)) {
             for (int q = 0; q < nInv; q++) {
@@ -659,7 +669,8 @@ int main(int argc, char **argv) {
   printf("{\"result\": \"%s\", \"generated\": %llu, \"distinct\": %llu, \"init\": %llu, \"depth\": %d, \"seconds\": %.6f",
          RESULT_NAME[result], (unsigned long long)generated, (unsigned long long)n_states,
          (unsigned long long)n_init, nlevels, secs);
-  if (result == R_OK) printf(", \"left_on_queue\": 0");
+  /* states left on queue: at an error, TLC's queue when it stopped */
+  printf(", \"left_on_queue\": %llu", (unsigned long long)(result == R_OK ? 0 : n_states - dequeued));
   if (print_levels) {
     printf(", \"levels\": [");
     for (int l = 0; l < nlevels; l++) printf("%s%llu", l ? ", " : "", (unsigned long long)(level_start[l + 1] - level_start[l]));

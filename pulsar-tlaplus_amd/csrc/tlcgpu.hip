@@ -629,6 +629,7 @@ struct tlcg_ctx {
   LevelCtr* h_aux = nullptr;
   // run state
   std::vector<u64> level_base;  // level_base[d] = gidx of the first state of level d
+  std::vector<u64> gen_at;      // gen_at[d] = generated before level d was expanded (TLC stop statistics)
   u64 generated = 0;
   int status = TLCG_RUNNING;
   u64 ev_word = NO_EVENT;
@@ -1614,6 +1615,7 @@ bool run_init(tlcg_ctx* c) {
   const HostModel& hm = c->hm;
   const Layout& L = hm.L;
   c->level_base.assign(1, 0);
+  c->gen_at.clear();
   c->generated = 0;
   c->status = TLCG_RUNNING;
   c->ev_word = NO_EVENT;
@@ -1836,6 +1838,8 @@ bool step_level(tlcg_ctx* c) {
   }
   u64 n_new = c->h_ctr->n_new;
   if (c->opts.fpset_spill && (n_new = tier_filter_level(c, d, n_new)) == ~0ull) return false;
+  c->gen_at.resize((size_t)depth - 1);
+  c->gen_at.push_back(c->generated);
   c->generated += c->h_ctr->generated;
   if (n_new) c->level_base.push_back(d + n_new);
   if (c->h_ctr->event != NO_EVENT) return resolve_event(c, c->h_ctr->event, depth);
@@ -2142,6 +2146,98 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
 
 }  // extern "C"
 
+// TLC's statistics at the moment a one-worker run stops on the error this
+// context found (tlcgpu.h).  TLC's Worker dequeues states in FIFO order and,
+// per state, runs the Next disjuncts in order: each action's successors are
+// generated as one StateVec and counted (statesGenerated += its size) before
+// any of them is put into the FPSet, enqueued and checked; the run stops at
+// the first violating new state, at a failing action (before its successors
+// are counted) or after all actions of a deadlocked state.  The global engine
+// in TLC order stores states in exactly that FIFO order, a level sorted by
+// first-discovery key (parent_gidx << ord_bits | ordinal), so:
+//   generated = gen_at[d] + outdeg(level-d states before p) + p's successors
+//               up to the stopping action;
+//   distinct  = states of levels <= d + level-(d+1) states discovered before
+//               the stop (a binary search over their parent references);
+//   left on queue = distinct - (p + 1)  (p and everything before it dequeued).
+int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, uint64_t* left_on_queue) {
+  const DeviceGuard dg(c);
+  if (!c) return -1;
+  if (c->status < TLCG_VIOLATION || !c->opts.tlc_order || c->opts.world != 1 || c->engine != TLCG_ENGINE_GLOBAL) {
+    c->err = "TLC stop statistics need a global-engine run in TLC order (world 1) that stopped on an error";
+    return -2;
+  }
+  const Layout& L = c->hm.L;
+  const u64 dkey = c->ev_word >> 6;
+  const int kind = (int)((c->ev_word >> 4) & 3);
+  if (c->ev_level == 0) {  // an initial state: Init enumeration index dkey, nothing dequeued yet
+    *generated = *distinct = *left_on_queue = dkey + 1;
+    return 0;
+  }
+  const size_t d = (size_t)c->ev_level - 1;  // level of the expanded state p
+  if (c->gen_at.size() <= d || c->level_base.size() <= d + 1) {
+    c->err = "TLC stop statistics are not available for a recovered run";
+    return -2;
+  }
+  const u64 pg = c->ev_parent_gidx;
+  const u64 f0 = c->level_base[d];
+  // successors of p counted before the stop: ordinals [0, lim)
+  const int a = c->ev_action;
+  const int lim = kind == EVK_DEADLOCK ? L.nkv + N_ACTIONS - 1
+                : kind == EVK_ACTION_ERROR ? ordinal_of(L, a, 0)
+                : (a == ACT_PRODUCER ? L.nkv : ordinal_of(L, a, 0) + 1);
+  u128 ps = 0;
+  u64 pp = 0;
+  if (!state_at(c, pg, &ps, &pp)) return -10;
+  u64 partial = 0;
+  for (int o = 0; o < lim; ++o) {
+    u128 t = 0;
+    partial += successor_at_any(c, ps, o, &t) == 1;
+  }
+  // out-degrees of the level-d states dequeued before p
+  const u64 n = pg - f0, w = c->words;
+  std::vector<u64> buf(std::max<u64>(n, 1) * w);
+  if (n && tlcg_copy_states_words(c, f0, n, buf.data()) != 0) return -10;
+  const int nt = (int)std::min<u64>(16, std::max<u64>(1, n / 65536));
+  std::vector<u64> part((size_t)nt, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      u64 acc = 0;
+      for (u64 i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+        if (w == 1) {
+          u64 out[80];
+          acc += (u64)host_successors<u64>(L, buf[i], out, nullptr, 80);
+        } else {
+          u128 out[80];
+          acc += (u64)host_successors<u128>(L, join_words(&buf[i * 2], 2), out, nullptr, 80);
+        }
+      }
+      part[(size_t)t] = acc;
+    });
+  for (auto& x : th) x.join();
+  u64 prefix = 0;
+  for (u64 x : part) prefix += x;
+  // level d + 1 (sorted by discovery key): states discovered before the stop
+  const u64 n1 = c->level_base[d + 1];
+  const u64 n2 = c->level_base.size() > d + 2 ? c->level_base[d + 2] : n1;
+  const u64 key_mask = (1ull << 56) - 1;
+  const u64 stop_key = kind == EVK_VIOLATION || kind == EVK_INV_ERROR ? dkey + 1 : (pg << L.ord_bits) | (u64)lim;
+  u64 lo = n1, hi = n2;  // first index whose discovery key >= stop_key
+  while (lo < hi) {
+    const u64 mid = lo + (hi - lo) / 2;
+    u128 s1 = 0;
+    u64 p1 = 0;
+    if (!state_at(c, mid, &s1, &p1)) return -10;
+    if ((p1 & key_mask) < stop_key) lo = mid + 1;
+    else hi = mid;
+  }
+  *generated = c->gen_at[d] + prefix + partial;
+  *distinct = lo;
+  *left_on_queue = lo - (pg + 1);
+  return 0;
+}
+
 // ---- checkpoint / recover (TLC -checkpoint / -recover) ----
 //
 // File: CkptHeader, the tlcg_model, level_base[n_levels], then the committed
@@ -2329,6 +2425,7 @@ int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
     return -10;
   }
   c->level_base = lb;
+  c->gen_at.clear();  // (not in the checkpoint: tlcg_tlc_stop_stats refuses after a recover)
   c->generated = h.generated;
   c->levels_redone = h.levels_redone;
   c->kernel_ms = h.kernel_ms;

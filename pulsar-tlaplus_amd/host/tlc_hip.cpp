@@ -264,6 +264,7 @@ int main(int argc, char** argv) {
     }
   }
   int rc = 0;
+  uint64_t stop_left = ~0ull;  // TLC's "states left on queue" at an error (tlcg_tlc_stop_stats)
   // PROPERTY Termination, checked like TLC after the safety search of the
   // complete state space ([TLC-ext] message text)
   int64_t live_idx = -1;
@@ -293,9 +294,12 @@ int main(int argc, char** argv) {
     tlcg_ctx* tctx = ctx;
     tlcg_stats tst = st;
     bool own = false;
-    if (o.trace && (!o.tlc_order || !ctx)) {  // (after -gpus N: on one GPU)
+    // (after -gpus N: on one GPU).  The global engine in TLC order stores the
+    // states in TLC's FIFO order, which also gives TLC's statistics at the stop.
+    if (o.trace && (!o.tlc_order || !ctx || st.engine != TLCG_ENGINE_GLOBAL)) {
       tlcg_opts to = opts;
       to.tlc_order = 1;
+      to.engine = TLCG_ENGINE_GLOBAL;
       if (!ctx) to.device = 0;
       if (tlcg_create(&model, &to, &tctx) == 0 && tlcg_run(tctx, &tst) == 0 && tst.status == st.status) {
         own = true;
@@ -343,11 +347,18 @@ int main(int argc, char** argv) {
         std::printf("Error: %s\n", tlcg_last_error(tctx));
       }
     }
+    // TLC stops mid-level: its counts at that moment (else the end of the level)
+    uint64_t sg = 0, sd = 0, sq = 0;
+    if (tctx && tlcg_tlc_stop_stats(tctx, &sg, &sd, &sq) == 0) {
+      st.generated = sg;
+      st.distinct = sd;
+      stop_left = sq;
+    }
     if (own) tlcg_destroy(tctx);
   }
   std::printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
               (unsigned long long)st.generated, (unsigned long long)st.distinct,
-              (unsigned long long)(st.status == TLCG_DONE ? 0 : st.frontier));
+              (unsigned long long)(st.status == TLCG_DONE ? 0 : stop_left != ~0ull ? stop_left : st.frontier));
   std::printf("The depth of the complete state graph search is %d.\n", st.depth);
   double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::printf("Finished in %s at (%s)\n", duration_str(secs).c_str(), now_str().c_str());

@@ -109,6 +109,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_trace_words": (C.c_int, [P, C.POINTER(U64), C.POINTER(I32), I32, C.POINTER(I32)]),
         "tlcg_state_at_words": (C.c_int, [P, U64, C.POINTER(U64), C.POINTER(U64)]),
         "tlcg_copy_states_words": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
+        "tlcg_tlc_stop_stats": (C.c_int, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
         "tlcg_absorb_records": (C.c_int, [P, P, U64, S]),
         "tlcg_stream": (P, [P]),
         "tlcg_peer_access": (C.c_int, [I32]),
@@ -357,6 +358,13 @@ class Checker:
         buf = (C.c_uint64 * (max(n, 1) * w))()
         self._chk(self.lib.tlcg_copy_states_words(self.ctx, first, n, buf), "tlcg_copy_states_words")
         return [_from_words(buf, i, w) for i in range(n)]
+
+    def tlc_stop_stats(self) -> Tuple[int, int, int]:
+        """(generated, distinct, left on queue) where a one-worker TLC run stops on
+        this error (tlcg_tlc_stop_stats; global engine, TLC order)."""
+        g, d, q = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.tlcg_tlc_stop_stats(self.ctx, C.byref(g), C.byref(d), C.byref(q)), "tlcg_tlc_stop_stats")
+        return g.value, d.value, q.value
 
     def state_at(self, gidx: int) -> Tuple[int, int]:
         s, p = (C.c_uint64 * 2)(), C.c_uint64()

@@ -111,6 +111,9 @@ def main():
                        (r["generated"], r["distinct"], r["depth"], r["levels"]), name
             else:
                 assert [a for a, _ in p["trace"]] == [t["action"] for t in r["trace"]], name
+                # TLC's counters where the one-worker run stops
+                assert (p["generated"], p["distinct"], p["left_on_queue"]) == \
+                       (r["generated"], r["distinct"], r["left_on_queue"]), name
         golden[name] = dict(constants=c, result=r)
         print(f"{name:24s} {r['result']:10s} gen={r['generated']} distinct={r.get('distinct')} depth={r.get('depth')}")
     assert golden["S"]["result"]["distinct"] == 45198            # compaction.tla:23

@@ -59,6 +59,41 @@ def test_golden_case(case, mode):
         assert r.engine == ("component" if fits else "global"), (r.engine, per_component)
 
 
+ERROR_CASES = [c for c in FULL_CASES if GOLDEN[c]["result"]["result"] != "ok"]
+
+
+@pytest.mark.parametrize("store", ["resident", "spilled"])
+@pytest.mark.parametrize("case", ERROR_CASES)
+def test_tlc_stop_statistics(case, store):
+    """TLC's "G states generated, D distinct states found, Q states left on
+    queue." where a one-worker run stops on the error (tlcg_tlc_stop_stats):
+    the oracles' stop point, with the levels in HBM or mostly spilled to host
+    memory (a 256-state device store)."""
+    m = model_of(GOLDEN[case]["constants"])
+    want = GOLDEN[case]["result"]
+    kw = dict(spill=True, device_store_cap=256) if store == "spilled" else {}
+    ck = tlcgpu.Checker(m, tlc_order=True, engine="global", **kw)
+    try:
+        r = ck.run()
+        assert r.status == want["result"]
+        assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"]), case
+    finally:
+        ck.close()
+
+
+def test_tlc_stop_statistics_need_tlc_order():
+    """Outside TLC order the store is not in TLC's FIFO order: refused."""
+    m = model_of(GOLDEN["V_leak"]["constants"])
+    for kw in (dict(engine="global"), dict(engine="component")):
+        ck = tlcgpu.Checker(m, **kw)
+        try:
+            assert ck.run().status == "invariant"
+            with pytest.raises(RuntimeError):
+                ck.tlc_stop_stats()
+        finally:
+            ck.close()
+
+
 def component_key_fits(c):
     """the component engine's admission rule: a one-word state whose part above
     `messages` (the local key) fits 32 bits (tlcgpu.hip component_applicable)"""
