@@ -129,6 +129,11 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
   __shared__ W s_st[STAGE_CAP];
   __shared__ u64 s_par[STAGE_CAP];
   __shared__ u64 s_slot[TLC ? STAGE_CAP : 1];
+  // PART: the stage also holds the records for other ranks; s_dst = the owner
+  // of each staged state (this rank for a new local state)
+  __shared__ uint8_t s_dst[PART ? STAGE_CAP : 1];
+  __shared__ unsigned s_dn[PART ? 64 : 1], s_dcur[PART ? 64 : 1];
+  __shared__ unsigned long long s_db[PART ? 64 : 1];
   __shared__ unsigned s_cnt;
   __shared__ unsigned long long s_base;
   const Layout& L = a.L;
@@ -144,35 +149,37 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
     u64 slot = 0;
     bool local = pred;
     if (PART) {
-      // successors owned elsewhere go to that rank's outbox.  The wave claims
-      // room with one atomic per destination, issued together by lanes
-      // 0..world-1 (a per-lane atomic on the world's few n_out words would
-      // serialize at the memory side)
+      // a successor owned elsewhere is staged with its owner and leaves for
+      // that rank's outbox at the block's flush, which claims room with one
+      // atomic per destination per block (per-wave claims on the world's few
+      // n_out words serialized at the memory side)
       const int dst = pred ? owner_of(t, a.owner_mask, a.world) : a.rank;
-      const bool remote = dst != a.rank;
+      const bool remote = pred && dst != a.rank;
       local = pred && !remote;
-      if (__ballot(remote)) {
-        const int lane = __lane_id();
-        u64 mine = 0;  // lane d: the lanes sending to destination d
-        for (int d = 0; d < a.world; ++d) {
-          const u64 m = __ballot(remote && dst == d);
-          if (lane == d) mine = m;
-        }
-        unsigned long long base = 0;
-        if (mine) base = atomicAdd(&a.ctr->n_out[lane], (unsigned long long)__popcll(mine));
-        const u64 m = __shfl((unsigned long long)mine, dst);
-        base = __shfl(base, dst);
-        if (remote) {
-          const unsigned long long pos = base + (unsigned long long)__popcll(m & lanemask_lt());
-          if (pos < a.outbox_cap) {
-            u64* rec = a.outbox + 2 * ((u64)dst * a.outbox_cap + pos);
-            rec[0] = (u64)t;  // PART: one-word states only (tlcg_create)
-            rec[1] = a.rank_tag | dkey;
-          } else {
-            atomicOr(&a.ctr->overflow, (unsigned)OVF_OUTBOX);
-          }
+      if (local) {
+        const int r = fpset_put(a.slots, a.log2, t, mixw(t), &slot);
+        if (r < 0) atomicOr(&a.ctr->overflow, ovf_of(r));
+        isnew = r == 1;
+        if (isnew) {
+          const int c = check_invariants(L, t);
+          if (c >= 0) ev = min(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
         }
       }
+      const bool put = remote || isnew;
+      const u64 m = __ballot(put);
+      if (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        unsigned base = 0;
+        if (__lane_id() == leader) base = atomicAdd(&s_cnt, (unsigned)__popcll(m));
+        base = __shfl(base, leader);
+        if (put) {
+          const unsigned pos = base + (unsigned)__popcll(m & lanemask_lt());
+          s_st[pos] = t;
+          s_par[pos] = a.rank_tag | dkey;
+          s_dst[pos] = (uint8_t)dst;
+        }
+      }
+      return;
     }
     if (local) {
       const int r = fpset_put(a.slots, a.log2, t, mixw(t), &slot);
@@ -189,6 +196,43 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
 
   auto flush = [&]() {
     __syncthreads();
+    if (PART) {
+      // counting sort of the stage by owner: one n_new / n_out claim per
+      // destination, then every state to the store or its rank's outbox
+      const unsigned n = s_cnt;
+      if (threadIdx.x < (unsigned)a.world) s_dn[threadIdx.x] = s_dcur[threadIdx.x] = 0;
+      __syncthreads();
+      for (unsigned i = threadIdx.x; i < n; i += BLOCK) atomicAdd(&s_dn[s_dst[i]], 1u);
+      __syncthreads();
+      if (threadIdx.x < (unsigned)a.world) {
+        const unsigned c = s_dn[threadIdx.x];
+        unsigned long long* ctr = (int)threadIdx.x == a.rank ? &a.ctr->n_new : &a.ctr->n_out[threadIdx.x];
+        s_db[threadIdx.x] = c ? atomicAdd(ctr, (unsigned long long)c) : 0;
+      }
+      __syncthreads();
+      for (unsigned i = threadIdx.x; i < n; i += BLOCK) {
+        const int d = s_dst[i];
+        const u64 pos = s_db[d] + atomicAdd(&s_dcur[d], 1u);
+        if (d == a.rank) {
+          if (pos < a.cap_out) {
+            reinterpret_cast<W*>(a.states_out)[pos] = s_st[i];
+            a.parents_out[pos] = s_par[i];
+          } else {
+            atomicOr(&a.ctr->overflow, (unsigned)OVF_STORE);
+          }
+        } else if (pos < a.outbox_cap) {
+          u64* rec = a.outbox + 2 * ((u64)d * a.outbox_cap + pos);
+          rec[0] = (u64)s_st[i];  // PART: one-word states only (tlcg_create)
+          rec[1] = s_par[i];
+        } else {
+          atomicOr(&a.ctr->overflow, (unsigned)OVF_OUTBOX);
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) s_cnt = 0;
+      __syncthreads();
+      return;
+    }
     if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&a.ctr->n_new, (unsigned long long)s_cnt) : 0;
     __syncthreads();
     const unsigned n = s_cnt;
