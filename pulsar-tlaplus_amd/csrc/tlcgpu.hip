@@ -522,33 +522,59 @@ __global__ __launch_bounds__(BLOCK) void k_mix_keys(const u64* __restrict__ stat
   if (i < n) keys[i] = mix64(states[i]);
 }
 
-// ---- world > 1: insert successors received from other ranks
+// ---- world > 1: insert successors received from other ranks.  Each thread
+// takes ABSORB_IT records and issues their first FPSet probes together (a
+// load each, then a CAS on the empty slots), as k_expand_fast does, so
+// ABSORB_IT scattered round trips are in flight per lane instead of one.
+constexpr int ABSORB_IT = 4;
 __global__ __launch_bounds__(BLOCK) void k_absorb(Layout L, const u64* __restrict__ recs, u64 n,
                                                   u64* __restrict__ slots, int log2, u64* __restrict__ states_out,
                                                   u64* __restrict__ parents_out, u64 cap, LevelCtr* ctr) {
-  __shared__ u64 s_st[BLOCK], s_par[BLOCK];
+  __shared__ u64 s_st[BLOCK * ABSORB_IT], s_par[BLOCK * ABSORB_IT];
   __shared__ unsigned s_cnt;
   __shared__ unsigned long long s_base;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
-  bool isnew = false;
-  u64 t = 0, ref = 0;
-  if (i < n) {
-    t = recs[2 * i];
-    ref = recs[2 * i + 1];
-    u64 slot;
-    const int r = fpset_put(slots, log2, t, mix64(t), &slot);
-    if (r < 0) atomicOr(&ctr->overflow, ovf_of(r));
-    isnew = r == 1;
-    if (isnew) {
-      const int c = check_invariants(L, t);
-      // keyed by inbox position, tagged with bit 57 (resolved on the host)
-      if (c >= 0)
-        atomicMin(&ctr->event, make_event((1ull << 51) | i, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
-    }
+  const u64 mask = (1ull << log2) - 1;
+  const u64 i0 = (u64)blockIdx.x * BLOCK * ABSORB_IT + threadIdx.x;
+  u64 t[ABSORB_IT], ref[ABSORB_IT], pos[ABSORB_IT], v[ABSORB_IT];
+  bool has[ABSORB_IT];
+#pragma unroll
+  for (int k = 0; k < ABSORB_IT; ++k) {
+    const u64 i = i0 + (u64)k * BLOCK;
+    has[k] = i < n;
+    t[k] = has[k] ? recs[2 * i] : 0;
+    ref[k] = has[k] ? recs[2 * i + 1] : 0;
+    pos[k] = mix64(t[k]) >> (64 - log2);
   }
-  stage_append<false, u64>(isnew, t, ref, 0, s_st, s_par, nullptr, &s_cnt);
+#pragma unroll
+  for (int k = 0; k < ABSORB_IT; ++k) v[k] = has[k] ? __builtin_nontemporal_load(&slots[pos[k]]) : 1;
+#pragma unroll
+  for (int k = 0; k < ABSORB_IT; ++k)
+    if (has[k] && v[k] == 0) v[k] = atomicCAS((unsigned long long*)&slots[pos[k]], 0ull, (unsigned long long)(t[k] | SLOT_TAG));
+#pragma unroll
+  for (int k = 0; k < ABSORB_IT; ++k) {
+    bool isnew = false;
+    if (has[k]) {
+      const u64 key = t[k] | SLOT_TAG;
+      if (v[k] == 0) {
+        isnew = true;
+      } else if (v[k] != key) {  // the first slot holds another state: probe on
+        u64 slot;
+        const int r = fpset_put_from(slots, mask, key, (pos[k] + 1) & mask, &slot);
+        if (r < 0) atomicOr(&ctr->overflow, (unsigned)OVF_FPSET);
+        isnew = r == 1;
+      }
+      if (isnew) {
+        const int c = check_invariants(L, t[k]);
+        // keyed by inbox position, tagged with bit 51 (resolved on the host)
+        if (c >= 0)
+          atomicMin(&ctr->event, make_event((1ull << 51) | (i0 + (u64)k * BLOCK), (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
+                                            c >> 1));
+      }
+    }
+    stage_append<false, u64>(isnew, t[k], ref[k], 0, s_st, s_par, nullptr, &s_cnt);
+  }
   __syncthreads();
   if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&ctr->n_new, (unsigned long long)s_cnt) : 0;
   __syncthreads();
@@ -2639,7 +2665,7 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
     return -10;
   for (;;) {
     if (hipEventRecord(c->e0, c->stream) != hipSuccess) return -10;
-    k_absorb<<<grid_for(n_records, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(
+    k_absorb<<<grid_for(n_records, (u64)BLOCK * ABSORB_IT, 0x7fffffffu), BLOCK, 0, c->stream>>>(
         c->hm.L, c->d_inbox, n_records, c->d_slots, c->log2, dev_state(c, d), dev_parent(c, d), dev_room(c, d),
         c->d_ctr);
     if (hipGetLastError() != hipSuccess) return -10;
