@@ -115,7 +115,10 @@ typedef struct tlcg_opts {
    * the filter says "maybe".  Counts, levels and traces are unchanged. */
   int32_t fpset_spill;
   int32_t log2_fpset_max;
-  int32_t reserved[2];
+  /* 1: keep TLC's outdegree histogram (tlcg_outdegree).  It costs the
+   * component kernel about 9 % on G9, so it is off unless asked for. */
+  int32_t outdegree;
+  int32_t reserved[1];
 } tlcg_opts;
 
 /* BFS engines.  GLOBAL: level-synchronous BFS over one HBM FPSet (64-bit CAS),
@@ -195,6 +198,14 @@ int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* ou
  * world 1); refused after tlcg_recover.  [TLC-ext: restated from TLC's
  * worker loop, not confirmable without TLC.] */
 int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, uint64_t* left_on_queue);
+/* TLC's outdegree statistics of a completed check ("The average outdegree of
+ * the complete state graph is M (minimum is A, the maximum B and the 95th
+ * percentile is P)."): hist[k] = states whose expansion discovered k new
+ * states (ModelChecker.doNext's unseenSuccessorStates, Worker.setOutDegree),
+ * *n = max k + 1.  Needs tlcg_opts.outdegree and TLC's first-discoverer
+ * parents: a global-engine run in TLC order (world 1) or the component
+ * engine; refused otherwise, and after tlcg_recover.  [TLC-ext] */
+int tlcg_outdegree(tlcg_ctx* c, uint64_t* hist, int32_t cap, int32_t* n);
 /* Successor ordinal bits (to split a parent_ref). */
 int tlcg_ordinal_bits(const tlcg_model* m);
 int tlcg_action_of_ordinal(const tlcg_model* m, int32_t ordinal);

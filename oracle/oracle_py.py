@@ -206,6 +206,7 @@ class Model:
                     return dict(result=b[0], invariant=b[1], generated=generated, distinct=len(states),
                                 left_on_queue=len(states), trace=trace(k))
         levels.append(len(states))
+        outdeg = {}  # new states discovered per expanded state (TLC's outdegree statistics)
         head = 0
         while head < len(states):
             end = len(states)
@@ -230,6 +231,7 @@ class Model:
                                 return stop(result=b[0], invariant=b[1], trace=trace(k))
                     return None
 
+                n_before = len(states)
                 pending = []
                 try:
                     for a, t in self.successors(s):
@@ -246,7 +248,11 @@ class Model:
                     return r
                 if n == 0 and self.deadlock:
                     return stop(result="deadlock", trace=trace(p))
+                k_new = len(states) - n_before
+                outdeg[k_new] = outdeg.get(k_new, 0) + 1
             head = end
             if len(states) > end:
                 levels.append(len(states) - end)
-        return dict(result="ok", generated=generated, distinct=len(states), depth=len(levels), levels=levels)
+        hist = [outdeg.get(i, 0) for i in range(max(outdeg) + 1)] if outdeg else []
+        return dict(result="ok", generated=generated, distinct=len(states), depth=len(levels), levels=levels,
+                    outdegree=hist)

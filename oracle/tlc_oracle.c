@@ -584,6 +584,10 @@ int main(int argc, char **argv) {
   int result = R_OK, bad_inv = -1;
   int64_t bad_parent = -1; int bad_action = -1; uint64_t dequeued = 0; St bad_state; memset(&bad_state, 0, sizeof bad_state);
   uint64_t level_start[4096]; int nlevels = 0;
+  /* TLC's outdegree statistics (ModelChecker.doNext: unseenSuccessorStates per
+     expanded state, Worker.setOutDegree): histogram of the number of new
+     states each dequeued state discovers */
+  static uint64_t outdeg[MAXK * MAXK + 16]; int max_outdeg = 0;
   fp_grow();
 
   /* ---- Init (compaction.tla:188-202) ---- */
@@ -627,7 +631,7 @@ int main(int argc, char **argv) {
     for (; head < lvl_end && result == R_OK; head++) {
       St s; load_state(head, &s);
       dequeued = head + 1;
-      int nsucc = 0;
+      int nsucc = 0, nnew = 0;
       /* Next, compaction.tla:216-231: disjuncts in source order */
       for (int a = 0; a < N_ACTIONS && result == R_OK; a++) {
         int cnt = 0, rc = EV_FALSE;
@@ -651,6 +655,7 @@ int main(int argc, char **argv) {
         for (int j = 0; j < cnt && result == R_OK; j++) {
           uint64_t k;
           if (fp_put(&out[j], (int64_t)head, a, &k)) {
+            nnew++;
             for (int q = 0; q < nInv; q++) {
               int v = eval_inv(Inv[q], &out[j]);
               if (v != EV_TRUE) { result = v == EV_ERROR ? R_INV_ERROR : R_INV; bad_inv = Inv[q]; bad_parent = (int64_t)head; bad_action = a; bad_state = out[j]; break; }
@@ -659,6 +664,8 @@ int main(int argc, char **argv) {
         }
       }
       if (result == R_OK && nsucc == 0 && CHECK_DEADLOCK) { result = R_DEADLOCK; bad_parent = (int64_t)head; bad_state = s; }
+      outdeg[nnew]++;
+      if (nnew > max_outdeg) max_outdeg = nnew;
     }
     if (n_states > lvl_end) { nlevels++; level_start[nlevels] = n_states; }
   }
@@ -671,6 +678,11 @@ int main(int argc, char **argv) {
          (unsigned long long)n_init, nlevels, secs);
   /* states left on queue: at an error, TLC's queue when it stopped */
   printf(", \"left_on_queue\": %llu", (unsigned long long)(result == R_OK ? 0 : n_states - dequeued));
+  if (result == R_OK) {
+    printf(", \"outdegree\": [");
+    for (int i = 0; i <= max_outdeg && n_states; i++) printf("%s%llu", i ? ", " : "", (unsigned long long)outdeg[i]);
+    printf("]");
+  }
   if (print_levels) {
     printf(", \"levels\": [");
     for (int l = 0; l < nlevels; l++) printf("%s%llu", l ? ", " : "", (unsigned long long)(level_start[l + 1] - level_start[l]));

@@ -42,6 +42,7 @@ struct CompArgs {
   unsigned long long* event;  // min event key (see make_comp_event)
   u64* ovf_list;               // components that did not fit: initial-state indices
   unsigned long long* ovf_n;
+  unsigned long long* outdeg;  // [3] expanded states that discovered 0 / 1 / 2 new states, or null (not counted)
 };
 
 // event key: level 8 | initial-state index 36 | queue position 8 | action 4 | kind 2 | index 4

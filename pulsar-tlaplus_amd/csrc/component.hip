@@ -8,9 +8,17 @@ namespace tlcg {
 
 namespace {
 
-template <int K>
+template <int K, bool OD>
 __global__ __launch_bounds__(64) void k_component(CompArgs a) {
-  component_body<K>(a, a.L);
+  component_body<K, OD>(a, a.L);
+}
+
+template <bool OD>
+void launch_k(const CompArgs& a, int K, unsigned grid, hipStream_t stream) {
+  if (K == 32) k_component<32, OD><<<grid, 64, 0, stream>>>(a);
+  else if (K == 64) k_component<64, OD><<<grid, 64, 0, stream>>>(a);
+  else if (K == 128) k_component<128, OD><<<grid, 64, 0, stream>>>(a);
+  else k_component<255, OD><<<grid, 64, 0, stream>>>(a);
 }
 
 }  // namespace
@@ -19,10 +27,8 @@ bool launch_component(const CompArgs& a, int K, hipStream_t stream) {
   if (!a.n_comp) return true;
   const u64 batches = (a.n_comp + 63) / 64;
   const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
-  if (K == 32) k_component<32><<<grid, 64, 0, stream>>>(a);
-  else if (K == 64) k_component<64><<<grid, 64, 0, stream>>>(a);
-  else if (K == 128) k_component<128><<<grid, 64, 0, stream>>>(a);
-  else k_component<255><<<grid, 64, 0, stream>>>(a);
+  if (a.outdeg) launch_k<true>(a, K, grid, stream);
+  else launch_k<false>(a, K, grid, stream);
   return hipGetLastError() == hipSuccess;
 }
 

@@ -25,8 +25,10 @@ template <int K>
 struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN + 15) / 16 * 16; };
 
 // the BFS of one wave's components; L is the runtime layout (precompiled
-// kernel) or a constexpr one (jit.cpp), in which case every field folds
-template <int K>
+// kernel) or a constexpr one (jit.cpp), in which case every field folds.
+// OD: also count TLC's outdegree histogram (a.outdeg; ~9 % of the kernel's
+// time on G9, so only when asked for, tlcg_opts.outdegree)
+template <int K, bool OD = false>
 __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& L) {
   constexpr int T = CompShape<K>::T;
   __shared__ uint32_t q[K][64];                   // FIFO of local keys (word >> msgs_bits)
@@ -36,6 +38,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
   const int mb = L.msg_sh + L.N * L.mw;  // `messages` occupies the low mb bits
   if (lane < COMP_MAXLV) lvl_sh[lane] = 0;
   u64 gen = 0, dist = 0;
+  unsigned od0 = 0, od1 = 0, od2 = 0;  // TLC's outdegree histogram: states with 0 / 1 / 2 new successors
   unsigned long long ev = NO_EVENT;
   __syncthreads();
   for (u64 b = blockIdx.x; b * 64 < a.n_comp; b += gridDim.x) {
@@ -61,6 +64,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     int head = 0, tail = 0, level = 0, lvl_end = 0, lvl_start = 0;
     bool alive = act, ovf = false;
     u64 lgen = 0;
+    unsigned ocnt = 0;  // this component's outdegree histogram, 10 bits per bin
     u64 lev = NO_EVENT;
     if (act) {
       const uint32_t k0 = (uint32_t)(s0 >> mb);
@@ -155,6 +159,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       }
       nsucc += selfloop_count_k(L, cmsg, s);  // Consumer / Terminating stutters
       lgen += (u64)nsucc;
+      if constexpr (OD) ocnt += 1u << (10 * (tail - tail0));  // new states this expansion discovered (0..2)
       if (alive && nsucc == 0 && L.check_deadlock) {
         lev = min(lev, make_comp_event(level + 1, idx0, head, 15, EVK_DEADLOCK, 0));
         alive = false;
@@ -181,6 +186,11 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     } else if (act) {
       gen += lgen;
       dist += (u64)tail;
+      if constexpr (OD) {
+        od0 += ocnt & 1023;
+        od1 += (ocnt >> 10) & 1023;
+        od2 += ocnt >> 20;
+      }
       ev = min(ev, (unsigned long long)lev);
       // a lane stopped by an error: `level` = [lvl_start, lvl_end) is partly
       // expanded and level+1 = [lvl_end, tail) partly discovered
@@ -193,6 +203,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
   }
   gen = wave_sum_u64(gen);
   dist = wave_sum_u64(dist);
+  const u64 o0 = wave_sum_u64(od0), o1 = wave_sum_u64(od1), o2 = wave_sum_u64(od2);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) ev = min(ev, (unsigned long long)__shfl_xor(ev, off));
   __syncthreads();
@@ -200,6 +211,11 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     if (gen) atomicAdd(&a.totals[0], (unsigned long long)gen);
     if (dist) atomicAdd(&a.totals[1], (unsigned long long)dist);
     if (ev != NO_EVENT) atomicMin(a.event, ev);
+    if constexpr (OD) {
+      if (o0) atomicAdd(&a.outdeg[0], (unsigned long long)o0);
+      if (o1) atomicAdd(&a.outdeg[1], (unsigned long long)o1);
+      if (o2) atomicAdd(&a.outdeg[2], (unsigned long long)o2);
+    }
   }
   if (lane < COMP_MAXLV && lvl_sh[lane]) atomicAdd(&a.lvl[lane], (unsigned long long)lvl_sh[lane]);
 }

@@ -53,8 +53,10 @@ std::string program_source(const Layout& L) {
   s += kJitSource;
   s += "\n" + layout_literal(L);
   for (int K : {32, 64, 128, 255})
-    s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_component_" + std::to_string(K) +
-         "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ">(a, kL); }\n";
+    for (const char* od : {"false", "true"})
+      s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_component_") +
+           (od[0] == 't' ? "od_" : "") + std::to_string(K) + "(tlcg::CompArgs a) { tlcg::component_body<" +
+           std::to_string(K) + ", " + od + ">(a, kL); }\n";
   return s;
 }
 
@@ -144,11 +146,14 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
     *err = "hipModuleLoadData failed for the specialized kernels";
     return false;
   }
-  const char* names[4] = {"tlcg_component_32", "tlcg_component_64", "tlcg_component_128", "tlcg_component_255"};
+  const char* names[4] = {"32", "64", "128", "255"};
   for (int i = 0; i < 4; ++i)
-    if (hipModuleGetFunction(&out->component[i], out->module, names[i]) != hipSuccess) {
-      *err = std::string("hipModuleGetFunction ") + names[i];
-      return false;
+    for (int od = 0; od < 2; ++od) {
+      const std::string n = std::string(od ? "tlcg_component_od_" : "tlcg_component_") + names[i];
+      if (hipModuleGetFunction(od ? &out->component_od[i] : &out->component[i], out->module, n.c_str()) != hipSuccess) {
+        *err = "hipModuleGetFunction " + n;
+        return false;
+      }
     }
   return true;
 }
@@ -161,11 +166,12 @@ void jit_release(JitKernels* k) {
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, hipStream_t stream) {
   if (!a.n_comp) return true;
   const int i = K == 32 ? 0 : K == 64 ? 1 : K == 128 ? 2 : 3;
+  hipFunction_t f = a.outdeg ? k.component_od[i] : k.component[i];
   const uint64_t batches = (a.n_comp + 63) / 64;
   const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
   CompArgs copy = a;
   void* args[] = {&copy};
-  return hipModuleLaunchKernel(k.component[i], grid, 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
+  return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
 }
 
 }  // namespace tlcg

@@ -13,7 +13,8 @@ namespace tlcg {
 
 struct JitKernels {
   hipModule_t module = nullptr;
-  hipFunction_t component[4] = {nullptr, nullptr, nullptr, nullptr};  // K = 32, 64, 128, 255
+  hipFunction_t component[4] = {nullptr, nullptr, nullptr, nullptr};     // K = 32, 64, 128, 255
+  hipFunction_t component_od[4] = {nullptr, nullptr, nullptr, nullptr};  // the same, counting outdegrees
   double compile_s = 0;  // 0 when loaded from the cache
   bool cached = false;
 };

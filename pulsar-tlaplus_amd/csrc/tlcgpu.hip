@@ -590,6 +590,22 @@ __global__ __launch_bounds__(BLOCK) void k_absorb(Layout L, const u64* __restric
   }
 }
 
+// TLC order: the new level is sorted by first-discovery key, so the states a
+// parent discovered first form one run of equal parent_gidx.  hist[len] +=
+// 1 for every run (len <= OUTDEG_BINS - 1: nkv + 2 new states per parent).
+constexpr int OUTDEG_BINS = 4100;
+__global__ __launch_bounds__(BLOCK) void k_child_runs(const u64* __restrict__ parents, u64 n, int ord_bits,
+                                                      unsigned long long* __restrict__ hist) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const u64 km = (1ull << 56) - 1;
+  const u64 p = (parents[i] & km) >> ord_bits;
+  if (i > 0 && ((parents[i - 1] & km) >> ord_bits) == p) return;  // not the start of a run
+  u64 len = 1;
+  while (i + len < n && ((parents[i + len] & km) >> ord_bits) == p) ++len;
+  atomicAdd(&hist[len < (u64)OUTDEG_BINS ? len : (u64)OUTDEG_BINS - 1], 1ull);
+}
+
 inline unsigned grid_for(u64 n, u64 per_block, unsigned cap) {
   u64 g = (n + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -700,6 +716,11 @@ struct tlcg_ctx {
   // run state
   std::vector<u64> level_base;  // level_base[d] = gidx of the first state of level d
   std::vector<u64> gen_at;      // gen_at[d] = generated before level d was expanded (TLC stop statistics)
+  // TLC's outdegree statistics: outdeg[k] = expanded states that discovered k
+  // new states; kept when the parent log is TLC's (TLC order, component engine)
+  std::vector<u64> outdeg;
+  bool outdeg_valid = false;
+  unsigned long long* d_runs = nullptr;  // [OUTDEG_BINS] device histogram of child runs
   u64 generated = 0;
   int status = TLCG_RUNNING;
   u64 ev_word = NO_EVENT;
@@ -1564,7 +1585,7 @@ bool component_applicable(const tlcg_ctx* c) {
 
 bool comp_scratch(tlcg_ctx* c, u64 n) {
   if (!c->d_comp) {
-    const size_t bytes = sizeof(unsigned long long) * (COMP_MAXLV + 4);
+    const size_t bytes = sizeof(unsigned long long) * (COMP_MAXLV + 7);
     if (!alloc_bytes(c, (void**)&c->d_comp, bytes, "component counters")) return false;
     HIPCHK(hipHostMalloc((void**)&c->h_comp, bytes));
   }
@@ -1593,6 +1614,8 @@ int run_component(tlcg_ctx* c) {
   c->passes.clear();
   c->comp_levels.assign(COMP_MAXLV, 0);
   c->comp_generated = c->comp_distinct = c->comp_store_used = 0;
+  c->outdeg.assign(3, 0);
+  c->outdeg_valid = c->opts.outdegree;  // the component engine's parents are TLC's first discoverers
   c->pending = 0;
   if (!comp_scratch(c, std::max<u64>(r1 - r0, 1))) return -1;
   // specialize the kernels for these constants when the run is large enough
@@ -1625,7 +1648,7 @@ int run_component(tlcg_ctx* c) {
       HIPCHK_I(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
     }
     const int out = cur == 0 ? 1 : 0;
-    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * (COMP_MAXLV + 4), c->stream));
+    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * (COMP_MAXLV + 7), c->stream));
     HIPCHK_I(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
     CompArgs a;
     a.L = L;
@@ -1641,6 +1664,7 @@ int run_component(tlcg_ctx* c) {
     a.totals = c->d_comp + COMP_MAXLV;
     a.event = c->d_comp + COMP_MAXLV + 2;
     a.ovf_n = c->d_comp + COMP_MAXLV + 3;
+    a.outdeg = c->opts.outdegree ? c->d_comp + COMP_MAXLV + 4 : nullptr;
     a.ovf_list = c->d_ovf[out];
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
     if (!(c->jit_used ? jit_launch_component(c->jit, a, K, c->stream) : launch_component(a, K, c->stream))) {
@@ -1648,7 +1672,7 @@ int run_component(tlcg_ctx* c) {
       return -1;
     }
     HIPCHK_I(hipEventRecord(c->e1, c->stream));
-    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * (COMP_MAXLV + 4),
+    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * (COMP_MAXLV + 7),
                           hipMemcpyDeviceToHost, c->stream));
     HIPCHK_I(hipStreamSynchronize(c->stream));
     float ms = 0;
@@ -1657,6 +1681,7 @@ int run_component(tlcg_ctx* c) {
     c->expand_ms += ms;
     for (int l = 0; l < COMP_MAXLV; ++l) c->comp_levels[(size_t)l] += c->h_comp[l];
     c->comp_generated += c->h_comp[COMP_MAXLV];
+    for (int i = 0; i < 3; ++i) c->outdeg[(size_t)i] += c->h_comp[COMP_MAXLV + 4 + i];
     c->comp_distinct += c->h_comp[COMP_MAXLV + 1];
     best_ev = std::min<u64>(best_ev, c->h_comp[COMP_MAXLV + 2]);
     c->comp_store_used = base + slots;
@@ -1686,6 +1711,8 @@ bool run_init(tlcg_ctx* c) {
   const Layout& L = hm.L;
   c->level_base.assign(1, 0);
   c->gen_at.clear();
+  c->outdeg.assign(1, 0);
+  c->outdeg_valid = c->opts.outdegree && c->opts.tlc_order && c->opts.world == 1;
   c->generated = 0;
   c->status = TLCG_RUNNING;
   c->ev_word = NO_EVENT;
@@ -1859,6 +1886,29 @@ u64 next_level_estimate(const tlcg_ctx* c, u64 F) {
   return (u64)(ratio * (double)F) + 1024;
 }
 
+// TLC's outdegree histogram from a finished TLC-order level: runs of equal
+// parent in the new level [d, d + n_new), the F - runs parents without one
+bool add_child_runs(tlcg_ctx* c, u64 d, u64 n_new, u64 F) {
+  std::vector<unsigned long long> h(OUTDEG_BINS, 0);
+  if (n_new) {
+    if (!c->d_runs && !alloc_bytes(c, (void**)&c->d_runs, OUTDEG_BINS * 8, "outdegree histogram")) return false;
+    HIPCHK(hipMemsetAsync(c->d_runs, 0, OUTDEG_BINS * 8, c->stream));
+    // the level sits in the device window unless a spill moved it (then it is
+    // the frontier of the next step, still on the device)
+    k_child_runs<<<grid_for(n_new, BLOCK, 0x7fffffffu), BLOCK, 0, c->stream>>>(dev_parent(c, d), n_new,
+                                                                              c->hm.L.ord_bits, c->d_runs);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h.data(), c->d_runs, OUTDEG_BINS * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  u64 runs = 0;
+  for (int k = 1; k < OUTDEG_BINS; ++k) runs += h[(size_t)k];
+  h[0] = F - runs;
+  if (c->outdeg.size() < (size_t)OUTDEG_BINS) c->outdeg.resize(OUTDEG_BINS, 0);
+  for (int k = 0; k < OUTDEG_BINS; ++k) c->outdeg[(size_t)k] += h[(size_t)k];
+  return true;
+}
+
 bool step_level(tlcg_ctx* c) {
   if (c->status != TLCG_RUNNING) return true;
   const HostModel& hm = c->hm;
@@ -1911,6 +1961,7 @@ bool step_level(tlcg_ctx* c) {
   c->gen_at.resize((size_t)depth - 1);
   c->gen_at.push_back(c->generated);
   c->generated += c->h_ctr->generated;
+  if (c->outdeg_valid && !add_child_runs(c, d, n_new, F)) return false;
   if (n_new) c->level_base.push_back(d + n_new);
   if (c->h_ctr->event != NO_EVENT) return resolve_event(c, c->h_ctr->event, depth);
   if (!n_new) c->status = TLCG_DONE;
@@ -2020,6 +2071,7 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_aux);
   jit_release(&c->jit);
   hipFree(c->d_comp);
+  hipFree(c->d_runs);
   hipFree(c->d_ovf[0]);
   hipFree(c->d_ovf[1]);
   if (c->h_comp) hipHostFree(c->h_comp);
@@ -2308,6 +2360,21 @@ int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, ui
   return 0;
 }
 
+// TLC's outdegree histogram of a completed check (tlcgpu.h)
+int tlcg_outdegree(tlcg_ctx* c, uint64_t* hist, int32_t cap, int32_t* n) {
+  if (!c || !n) return -1;
+  if (c->status != TLCG_DONE || !c->outdeg_valid) {
+    c->err = "the outdegree histogram needs tlcg_opts.outdegree and a completed check in TLC order or on the "
+             "component engine";
+    return -2;
+  }
+  size_t m = c->outdeg.size();
+  while (m && c->outdeg[m - 1] == 0) --m;
+  *n = (int32_t)m;
+  for (size_t i = 0; i < m && (int32_t)i < cap; ++i) hist[i] = c->outdeg[i];
+  return 0;
+}
+
 // ---- checkpoint / recover (TLC -checkpoint / -recover) ----
 //
 // File: CkptHeader, the tlcg_model, level_base[n_levels], then the committed
@@ -2496,6 +2563,7 @@ int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
   }
   c->level_base = lb;
   c->gen_at.clear();  // (not in the checkpoint: tlcg_tlc_stop_stats refuses after a recover)
+  c->outdeg_valid = false;  // (nor the outdegree histogram of the levels before it)
   c->generated = h.generated;
   c->levels_redone = h.levels_redone;
   c->kernel_ms = h.kernel_ms;

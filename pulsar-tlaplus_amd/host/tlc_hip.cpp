@@ -206,6 +206,7 @@ int main(int argc, char** argv) {
   // memory when HBM runs short (never otherwise)
   opts.spill = 1;
   opts.fpset_spill = tlcg_state_words(&model) == 1;  // and TLC's DiskFPSet: the host tier (narrow states)
+  opts.outdegree = 1;  // TLC's outdegree line
   if (!recover_file.empty()) opts.engine = TLCG_ENGINE_GLOBAL;  // checkpoints are global-engine level states
   else std::printf("Computing initial states...\n");
   tlcg_ctx* ctx = nullptr;
@@ -360,6 +361,26 @@ int main(int argc, char** argv) {
               (unsigned long long)st.generated, (unsigned long long)st.distinct,
               (unsigned long long)(st.status == TLCG_DONE ? 0 : stop_left != ~0ull ? stop_left : st.frontier));
   std::printf("The depth of the complete state graph search is %d.\n", st.depth);
+  // TLC's outdegree line (complete searches; needs TLC's first-discoverer parents)
+  std::vector<uint64_t> od(4100);
+  int32_t nod = 0;
+  if (ctx && st.status == TLCG_DONE && tlcg_outdegree(ctx, od.data(), (int32_t)od.size(), &nod) == 0 && nod > 0) {
+    // BucketStatistics: mean rounded; the 95th percentile is the first bucket
+    // whose cumulative count reaches 0.95 of the observations
+    uint64_t total = 0, weighted = 0, cum = 0;
+    int mn = -1, p95 = 0;
+    for (int k = 0; k < nod; ++k) {
+      total += od[(size_t)k];
+      weighted += (uint64_t)k * od[(size_t)k];
+      if (mn < 0 && od[(size_t)k]) mn = k;
+    }
+    for (int k = 0; k < nod; ++k) {
+      cum += od[(size_t)k];
+      if ((double)cum >= 0.95 * (double)total) { p95 = k; break; }
+    }
+    std::printf("The average outdegree of the complete state graph is %lld (minimum is %d, the maximum %d and the 95th percentile is %d).\n",
+                (long long)std::llround((double)weighted / (double)total), mn, nod - 1, p95);
+  }
   double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::printf("Finished in %s at (%s)\n", duration_str(secs).c_str(), now_str().c_str());
   if (o.json) {

@@ -44,7 +44,8 @@ class tlcg_opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("log2_fpset_slots", C.c_int32), ("state_capacity", C.c_uint64),
                 ("tlc_order", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32), ("partition", C.c_int32),
                 ("engine", C.c_int32), ("spill", C.c_int32), ("device_store_cap", C.c_uint64),
-                ("fpset_spill", C.c_int32), ("log2_fpset_max", C.c_int32), ("reserved", C.c_int32 * 2)]
+                ("fpset_spill", C.c_int32), ("log2_fpset_max", C.c_int32), ("outdegree", C.c_int32),
+                ("reserved", C.c_int32 * 1)]
 
 
 class tlcg_stats(C.Structure):
@@ -110,6 +111,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_state_at_words": (C.c_int, [P, U64, C.POINTER(U64), C.POINTER(U64)]),
         "tlcg_copy_states_words": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
         "tlcg_tlc_stop_stats": (C.c_int, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
+        "tlcg_outdegree": (C.c_int, [P, C.POINTER(U64), I32, C.POINTER(I32)]),
         "tlcg_absorb_records": (C.c_int, [P, P, U64, S]),
         "tlcg_stream": (P, [P]),
         "tlcg_peer_access": (C.c_int, [I32]),
@@ -282,7 +284,7 @@ class Checker:
     def __init__(self, model: Model, device: int = 0, log2_fpset_slots: int = 0, state_capacity: int = 0,
                  tlc_order: bool = False, rank: int = 0, world: int = 1, partition: int = 0,
                  engine: str = "auto", spill: bool = False, device_store_cap: int = 0,
-                 fpset_spill: bool = False, log2_fpset_max: int = 0):
+                 fpset_spill: bool = False, log2_fpset_max: int = 0, outdegree: bool = False):
         self.lib = load_library()
         self.model = model
         self._m = model.to_c()
@@ -292,6 +294,7 @@ class Checker:
         o.engine = ENGINES[engine]
         o.spill, o.device_store_cap = int(spill), device_store_cap
         o.fpset_spill, o.log2_fpset_max = int(fpset_spill), log2_fpset_max
+        o.outdegree = int(outdegree)
         self._o = o
         self.ctx = C.c_void_p()
         rc = self.lib.tlcg_create(C.byref(self._m), C.byref(o), C.byref(self.ctx))
@@ -365,6 +368,14 @@ class Checker:
         g, d, q = C.c_uint64(), C.c_uint64(), C.c_uint64()
         self._chk(self.lib.tlcg_tlc_stop_stats(self.ctx, C.byref(g), C.byref(d), C.byref(q)), "tlcg_tlc_stop_stats")
         return g.value, d.value, q.value
+
+    def outdegree(self) -> List[int]:
+        """TLC's outdegree histogram of the completed check (tlcg_outdegree):
+        [k] = states whose expansion discovered k new states."""
+        buf = (C.c_uint64 * 4100)()
+        n = C.c_int32()
+        self._chk(self.lib.tlcg_outdegree(self.ctx, buf, 4100, C.byref(n)), "tlcg_outdegree")
+        return [buf[i] for i in range(n.value)]
 
     def state_at(self, gidx: int) -> Tuple[int, int]:
         s, p = (C.c_uint64 * 2)(), C.c_uint64()

@@ -107,8 +107,8 @@ def main():
             p = py_check(c)
             assert p["result"] == r["result"], (name, p["result"], r["result"])
             if r["result"] == "ok":
-                assert (p["generated"], p["distinct"], p["depth"], p["levels"]) == \
-                       (r["generated"], r["distinct"], r["depth"], r["levels"]), name
+                assert (p["generated"], p["distinct"], p["depth"], p["levels"], p["outdegree"]) == \
+                       (r["generated"], r["distinct"], r["depth"], r["levels"], r["outdegree"]), name
             else:
                 assert [a for a, _ in p["trace"]] == [t["action"] for t in r["trace"]], name
                 # TLC's counters where the one-worker run stops

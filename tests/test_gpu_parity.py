@@ -81,6 +81,32 @@ def test_tlc_stop_statistics(case, store):
         ck.close()
 
 
+OK_CASES = [c for c in FULL_CASES if GOLDEN[c]["result"]["result"] == "ok"]
+
+
+@pytest.mark.parametrize("mode", ["auto", "tlc_order"])
+@pytest.mark.parametrize("case", OK_CASES)
+def test_outdegree_histogram(case, mode):
+    """TLC's outdegree statistics (new states discovered per expanded state,
+    over TLC's first-discoverer tree) against both oracles' histogram: from the
+    component engine's lanes, or from the runs of equal parent in every sorted
+    TLC-order level.  The global engine in fast order refuses (its parents are
+    whichever insert won)."""
+    m = model_of(GOLDEN[case]["constants"])
+    ck = tlcgpu.Checker(m, tlc_order=mode == "tlc_order", engine="global" if mode == "tlc_order" else "auto",
+                        outdegree=True)
+    try:
+        r = ck.run()
+        assert r.status == "ok"
+        if mode == "tlc_order" or r.engine == "component":
+            assert ck.outdegree() == GOLDEN[case]["result"]["outdegree"], (case, mode, r.engine)
+        else:
+            with pytest.raises(RuntimeError):
+                ck.outdegree()
+    finally:
+        ck.close()
+
+
 def test_tlc_stop_statistics_need_tlc_order():
     """Outside TLC order the store is not in TLC's FIFO order: refused."""
     m = model_of(GOLDEN["V_leak"]["constants"])

@@ -2,7 +2,8 @@
 oracle run live on the same inputs (oracle/build/tlc_oracle, the checker).
 Counts, per-level sizes, depth and verdict through the default engine and the
 global engine in TLC order; on an error, TLC's trace text and TLC's
-statistics at the stop (tlcg_tlc_stop_stats).
+statistics at the stop (tlcg_tlc_stop_stats); on success, TLC's outdegree
+histogram (tlcg_outdegree).
 
 The draws cover every knob of compaction.cfg: MessageSentLimit 0..3,
 CompactionTimesLimit 1..6 (wide > 63-bit layouts included), MaxCrashTimes
@@ -44,13 +45,16 @@ def test_random_cfg_matches_oracle(seed):
         pytest.skip(f"constants refused: {tlcgpu.check_model(m)}")
     want = run_oracle(m)
     for mode in ("auto", "tlc_order"):
-        ck = tlcgpu.Checker(m, tlc_order=mode == "tlc_order", engine="auto" if mode == "auto" else "global")
+        ck = tlcgpu.Checker(m, tlc_order=mode == "tlc_order", engine="auto" if mode == "auto" else "global",
+                            outdegree=True)
         try:
             r = ck.run()
             assert r.status == want["result"], (seed, mode, r.status, want["result"])
             if want["result"] == "ok":
                 assert (r.generated, r.distinct, r.depth, r.levels) == \
                        (want["generated"], want["distinct"], want["depth"], want["levels"]), (seed, mode)
+                if mode == "tlc_order" or r.engine == "component":  # TLC's first-discoverer tree
+                    assert ck.outdegree() == want["outdegree"], (seed, mode)
                 continue
             assert r.depth == want["depth"], (seed, mode)
             if want["result"] in ("invariant", "invariant_error"):
