@@ -38,15 +38,27 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_STATE_WORD = 8
 
 
-PMC_PROFILE = "profiles/r01_pmc_k_expand.json"
-PMC_COMPONENT_PROFILE = "profiles/r01_pmc_component.json"
+# the newest round's profile of each kind (profiles/rNN_*), measured on the same kernels
+PMC_PROFILE = "pmc_k_expand.json"
+PMC_COMPONENT_PROFILE = "pmc_component.json"
 COMPONENT_BYTES_PER_STATE = 16  # state word + parent entry written to the HBM store
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
+# algorithmic HBM bytes per distinct state of the BFS path (read
+# the frontier state 8 B, write the new state 8 B and its parent entry 8 B,
+# g/d = 1.339 probes of 8 B); roofline.achieved prices every engine with it
+SURVEY_BYTES_PER_DISTINCT = 34.7
+# MI355X issue model for roofline.issue (MI355X_MICROARCH.md): 256 CUs x 4
+# SIMD-32; a wave64 VALU instruction takes 2 cycles of its SIMD, the CU's one
+# scalar unit issues one SALU instruction per cycle, SQ_LDS_IDX_ACTIVE counts
+# LDS-array cycles (one array per CU); 2.4 GHz
+CUS, SIMDS, CLOCK_HZ = 256, 4, 2.4e9
 
 
-def load_profile(rel):
-    p = os.path.join(ROOT, rel)
-    return json.load(open(p)) if os.path.exists(p) else None
+def load_profile(name):
+    """profiles/<newest round>_<name>, or None"""
+    import glob
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_" + name)))
+    return json.load(open(hits[-1])) | {"_file": os.path.relpath(hits[-1], ROOT)} if hits else None
 
 
 def load_microbench(rel):
@@ -290,7 +302,8 @@ def main():
 
     def roofline_global(r):
         abytes = algorithmic_bytes(distinct, generated, n_init, selfloops, words)
-        bytes_step = abytes / world  # per rank
+        # SURVEY 8(d)'s per-unit figure x the units (distinct states) of one step, per rank
+        bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
@@ -298,13 +311,15 @@ def main():
                                              "k_expand<u64, Producer>" if words == 1 else
                                              "k_expand<u128> (wide FPSet)"),
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=round(abytes / distinct, 2))
+                  bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
+                  kernel_bytes_per_distinct=round(abytes / distinct, 2))
         pmc = load_profile(PMC_PROFILE)
         avg_launch_s = r["expand_ms"] / r["launches"] * 1e-3
-        if pmc and args.config == "g9" and world == 1:
+        if pmc and args.config == "g9" and world == 1 and words == 1 and not open_model:
             rf["traffic"] = round(pmc["hbm_bytes_per_launch"] / avg_launch_s / 1e9, 1)
             rf["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_launch"])
-            rf["traffic_source"] = PMC_PROFILE
+            rf["traffic_over_algorithmic"] = round(pmc["hbm_bytes_per_launch"] * r["launches"] / abytes, 2)
+            rf["traffic_source"] = pmc["_file"]
         micro = load_microbench(MICRO_PROFILE)
         if micro and words == 1:
             probes = (generated - n_init - selfloops) / world
@@ -317,22 +332,40 @@ def main():
         return rf
 
     def roofline_component(r):
-        # the component kernel's only HBM traffic: write each state word and its parent entry
-        bytes_step = COMPONENT_BYTES_PER_STATE * distinct / world
+        # SURVEY 8(d)'s per-unit figure x the distinct states of one launch; the
+        # kernel itself only writes 16 B/state (the FPSet and queue stay on chip)
+        bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
+        written = COMPONENT_BYTES_PER_STATE * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
                   kernel="tlcg_component_64 (hipRTC-specialized)" if r["jit"] else "k_component<64>",
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=COMPONENT_BYTES_PER_STATE)
+                  bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
+                  kernel_bytes_per_distinct=COMPONENT_BYTES_PER_STATE,
+                  kernel_written_gbs=round(written, 1))
         pmc = load_profile(PMC_COMPONENT_PROFILE)
         if pmc and args.config == "g9" and world == 1 and r["jit"]:
-            rf["traffic"] = round(pmc["hbm_bytes_per_step"] / (r["expand_ms"] * 1e-3) / 1e9, 1)
+            c = pmc["counters"]
+            kt = r["expand_ms"] * 1e-3
+            rf["traffic"] = round(pmc["hbm_bytes_per_step"] / kt / 1e9, 1)
             rf["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_step"])
-            rf["traffic_source"] = PMC_COMPONENT_PROFILE
-            rf["issue"] = dict(valu_insts_per_state=round(pmc["valu_insts_per_state"], 1),
-                               salu_insts_per_state=round(pmc["salu_insts_per_state"], 1),
-                               note="issue/latency-bound on chip (LDS FPSet), not HBM-bound")
+            rf["traffic_source"] = pmc["_file"]
+            # issue bound: each port's busy time at full rate / the kernel's time
+            t_valu = c["SQ_INSTS_VALU"] * 2 / (CUS * SIMDS * CLOCK_HZ)
+            t_salu = c["SQ_INSTS_SALU"] / (CUS * CLOCK_HZ)
+            t_lds = c["SQ_LDS_IDX_ACTIVE"] / (CUS * CLOCK_HZ)
+            t_sum = (c["SQ_INSTS_VALU"] + c["SQ_INSTS_SALU"] + c["SQ_INSTS_LDS"]) / (CUS * SIMDS * CLOCK_HZ)
+            rf["issue"] = dict(
+                frac=round(max(t_valu, t_salu, t_lds) / kt, 3),
+                frac_all_ports_one_issue=round(t_sum / kt, 3),
+                valu_ms=round(t_valu * 1e3, 3), salu_ms=round(t_salu * 1e3, 3), lds_ms=round(t_lds * 1e3, 3),
+                valu_wave_insts_per_state=round(c["SQ_INSTS_VALU"] / distinct, 3),
+                salu_wave_insts_per_state=round(c["SQ_INSTS_SALU"] / distinct, 3),
+                lds_wave_insts_per_state=round(c["SQ_INSTS_LDS"] / distinct, 3),
+                wave_issue_frac=round(pmc["wave_issue_frac"], 3),
+                formula="frac = max(VALU x 2 cyc / (256 CU x 4 SIMD), SALU x 1 cyc / 256 CU, "
+                        "SQ_LDS_IDX_ACTIVE / 256 CU) / 2.4 GHz / kernel time (DESIGN 4)")
         return rf
 
     def summary(r):

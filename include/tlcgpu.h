@@ -206,6 +206,13 @@ int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, ui
  * parents: a global-engine run in TLC order (world 1) or the component
  * engine; refused otherwise, and after tlcg_recover.  [TLC-ext] */
 int tlcg_outdegree(tlcg_ctx* c, uint64_t* hist, int32_t cap, int32_t* n);
+/* States generated per BFS level: out[0] = the initial states, out[k] = the
+ * successors generated by expanding level k - 1 (stutters included), *n =
+ * expanded levels + 1.  The sum is tlcg_stats.generated; the sum of
+ * out[0..E] is the count at the end of level E (what combining ranks that
+ * stopped at different levels needs, tlcg_run_node / dist.py).  Refused after
+ * tlcg_recover (the checkpoint holds only the total). */
+int tlcg_level_generated(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n);
 /* Successor ordinal bits (to split a parent_ref). */
 int tlcg_ordinal_bits(const tlcg_model* m);
 int tlcg_action_of_ordinal(const tlcg_model* m, int32_t ordinal);

@@ -109,6 +109,11 @@ class Model:
                     l2[old - 1] = None
                     nl = tuple(l2)
             yield 6, (msgs, nl, cur, P1, None, hz, ctx, crash, cons)
+        yield from self.tail_actions(s)
+
+    def tail_actions(self, s):
+        """The disjuncts after the compactor's (:227-230), which never fail."""
+        msgs, led, cur, ph, p1r, hz, ctx, crash, cons = s
         if crash < self.K:  # BrokerCrash, :169-182
             h, c = cur if cur is not None else (0, 0)
             yield 7, (msgs, led, cur, P1, None, h, c, crash + 1, cons)
@@ -142,19 +147,18 @@ class Model:
                     and (cur is None or (1 <= cur[0] <= N and 1 <= cur[1] <= C)))
         if name == "CompactedLedgerLeak":  # :253
             return sum(l is not None for l in led) <= 2
-        if name == "CompactionHorizonCorrectness":  # :259-274
+        if name == "CompactionHorizonCorrectness":  # :259-274, literally
+            # Len(messagesBeforeHorizon) (:269) enumerates the function, so every
+            # messages[i], i <= hz, is evaluated before the first i is tested
+            if hz > len(msgs):
+                raise EvalError("messages[i]")
             for i in range(1, hz + 1):
-                if i > len(msgs):
-                    raise EvalError("messages[i]")
                 m = msgs[i - 1]
                 if m[1] == 0 and not self.retain:
-                    continue
+                    continue  # messagesBeforeHorizon[i] = Nil: FALSE => ... holds (:271)
                 L = self.ledger_at_ctx(s)
-                if m[1] == 0:
-                    found = any(e == m for e in L)
-                else:
-                    found = any(e[1] == m[1] and e[0] >= m[0] for e in L)
-                if not found:
+                # ELSE branch (:272-274), a retained null-key message included
+                if not any(e[1] == m[1] and e[0] >= m[0] for e in L):
                     return False
             return True
         if name == "DuplicateNullKeyMessage":  # :280-294
@@ -197,25 +201,50 @@ class Model:
                 out.append(extra)
             return out
 
+        def end_of_level(first, last):
+            """The counts of a level-synchronous checker that finishes the level
+            [first, last) it was expanding: every state expanded, every successor
+            of every action that does not fail counted and inserted."""
+            gen = gen_at_level
+            for q in range(first, last):
+                succ = []
+                try:
+                    for x in self.successors(states[q]):
+                        succ.append(x)
+                except EvalError:  # a failing compactor disjunct: the later ones still run
+                    succ += list(self.tail_actions(states[q]))
+                gen += len(succ)
+                for a, t in succ:
+                    add(t, q, ACTIONS[a])
+            return gen, len(states)
+
+        gen_at_level = 0
         for t in self.inits():
             generated += 1
             k = add(t, -1, "Init")
             if k is not None:
                 b = bad(t)
                 if b:
-                    return dict(result=b[0], invariant=b[1], generated=generated, distinct=len(states),
-                                left_on_queue=len(states), trace=trace(k))
+                    r = dict(result=b[0], invariant=b[1], generated=generated, distinct=len(states),
+                             left_on_queue=len(states), trace=trace(k))
+                    for t2 in self.inits():  # end of level 0: every initial state
+                        add(t2, -1, "Init")
+                    r["eol_generated"], r["eol_distinct"] = sum(1 for _ in self.inits()), len(states)
+                    return r
         levels.append(len(states))
         outdeg = {}  # new states discovered per expanded state (TLC's outdegree statistics)
         head = 0
         while head < len(states):
             end = len(states)
+            gen_at_level = generated
             for p in range(head, end):
                 s = states[p]
                 n = 0
 
                 def stop(**kw):  # TLC's counters when the run stops while expanding p
-                    return dict(generated=generated, distinct=len(states), left_on_queue=len(states) - (p + 1), **kw)
+                    r = dict(generated=generated, distinct=len(states), left_on_queue=len(states) - (p + 1), **kw)
+                    r["eol_generated"], r["eol_distinct"] = end_of_level(head, end)
+                    return r
 
                 def process(group):
                     """one action's successors: counted as a whole (TLC's StateVec),

@@ -420,20 +420,28 @@ static int ledger_at_ctx(const St *s, int *idx) {
   return EV_TRUE;
 }
 
-/* CompactionHorizonCorrectness, compaction.tla:259-274 */
+/* CompactionHorizonCorrectness, compaction.tla:259-274, read literally.
+   Len(messagesBeforeHorizon) (:269) turns the function [i \in 1..hz |-> ...]
+   into a tuple, which evaluates messages[i] for every i <= hz first: an i
+   past Len(messages) is an evaluation error before any i is tested
+   ([TLC-ext]: TLC's Len on a function constructor enumerates it).
+   messagesBeforeHorizon[i] is Nil only for a null key without RetainNullKey
+   (:263-266); then the THEN branch `RetainNullKey => ...` (:271) holds
+   without evaluating its right side.  Every other message -- a retained
+   null-key one included -- takes the ELSE branch (:272-274): some ledger
+   entry with the same key and an id >= the message's. */
 static int inv_horizon(const St *s) {
+  if (s->hz > s->nmsg) { snprintf(g_errmsg, sizeof g_errmsg, "messages[%d] out of domain", s->nmsg + 1); return EV_ERROR; }
   for (int i = 1; i <= s->hz; i++) { /* \A i \in 1..Len(messagesBeforeHorizon), in order */
-    if (i > s->nmsg) { snprintf(g_errmsg, sizeof g_errmsg, "messages[%d] out of domain", i); return EV_ERROR; }
     const Msg *mi = &s->msgs[i - 1];
-    int isNil = (mi->key == NullKey) && !RETAIN; /* messagesBeforeHorizon[i] */
+    int isNil = (mi->key == NullKey) && !RETAIN; /* messagesBeforeHorizon[i] = Nil */
     if (isNil) continue;                          /* RetainNullKey => ... is TRUE */
     int L;
     if (ledger_at_ctx(s, &L) == EV_ERROR) return EV_ERROR;
     int found = 0;
     for (int j = 0; j < s->led_len[L] && !found; j++) {
       const Msg *e = &s->led[L][j];
-      if (mi->key == NullKey) found = msg_eq(e, mi);          /* RETAIN: exact record match */
-      else found = (e->key == mi->key && e->id >= mi->id);
+      found = (e->key == mi->key && e->id >= mi->id);
     }
     if (!found) return EV_FALSE;
   }
@@ -619,6 +627,7 @@ int main(int argc, char **argv) {
       }
     }
   }
+  uint64_t eol_generated = 0, eol_distinct = 0;
   uint64_t n_init = n_states;
   nlevels = 1;
   level_start[1] = n_states;
@@ -626,8 +635,10 @@ int main(int argc, char **argv) {
   /* ---- BFS: FIFO over the store (store order == queue order) ---- */
   static St succ[MAXK * MAXK + 16];
   uint64_t head = 0;
+  uint64_t lvl_first = 0, lvl_last = 0, gen_at_level = 0;
   while (result == R_OK && head < n_states) {
     uint64_t lvl_end = n_states; /* current level [head, lvl_end) */
+    lvl_first = head; lvl_last = lvl_end; gen_at_level = generated;
     for (; head < lvl_end && result == R_OK; head++) {
       St s; load_state(head, &s);
       dequeued = head + 1;
@@ -670,14 +681,68 @@ int main(int argc, char **argv) {
     if (n_states > lvl_end) { nlevels++; level_start[nlevels] = n_states; }
   }
 
+  /* End-of-level counts at an error (not TLC's: TLC stops mid-level, above).
+     A level-synchronous checker finishes the level it was expanding: every
+     state of [lvl_first, lvl_last) expanded, every successor of every action
+     that does not fail counted and inserted, invariants no longer checked.
+     These are the counts such a checker reports at the error. */
+  const uint64_t tlc_distinct = n_states;  /* where TLC stopped (printed below) */
+  /* end-of-level counts at an error in Init: every initial state inserted */
+  if (result != R_OK && bad_parent == -2) {
+    long long total = 1;
+    if (!PRODUCER) for (int i = 0; i < N; i++) total *= (long long)(nKeySet * nValueSet);
+    eol_generated = (uint64_t)(init_hi - init_lo);
+    for (long long idx = init_lo; idx < init_hi; idx++) {
+      St s; init_state(&s);
+      if (!PRODUCER) {
+        long long r = idx;
+        s.nmsg = N;
+        for (int i = 0; i < N; i++) {
+          int d = (int)(r % (nKeySet * nValueSet)); r /= (nKeySet * nValueSet);
+          s.msgs[i].id = i + 1; s.msgs[i].key = KeySet[d % nKeySet]; s.msgs[i].value = ValueSet[d / nKeySet];
+        }
+      }
+      uint64_t k;
+      fp_put(&s, -1, A_INIT, &k);
+    }
+    eol_distinct = n_states;
+    (void)total;
+  }
+  if (result != R_OK && bad_parent >= 0) {
+    eol_generated = gen_at_level;
+    for (uint64_t p = lvl_first; p < lvl_last; p++) {
+      St s; load_state(p, &s);
+      for (int a = 0; a < N_ACTIONS; a++) {
+        int cnt = 0, rc = EV_FALSE;
+        St *out = succ;
+        switch (a) {
+          case A_PRODUCER: if (PRODUCER) rc = act_producer(&s, out, &cnt); break;
+          case A_PHASEONE: rc = act_phase_one(&s, out); cnt = rc == EV_TRUE; break;
+          case A_WRITE: rc = act_write(&s, out); cnt = rc == EV_TRUE; break;
+          case A_UCTX: rc = act_update_context(&s, out); cnt = rc == EV_TRUE; break;
+          case A_UHOR: rc = act_update_horizon(&s, out); cnt = rc == EV_TRUE; break;
+          case A_PERSIST: rc = act_persist(&s, out); cnt = rc == EV_TRUE; break;
+          case A_DELETE: rc = act_delete(&s, out); cnt = rc == EV_TRUE; break;
+          case A_CRASH: rc = act_crash(&s, out); cnt = rc == EV_TRUE; break;
+          case A_CONSUMER: if (CONSUMER) { out[0] = s; cnt = 1; } break;
+          case A_TERMINATING: if (enabled_terminating(&s)) { out[0] = s; cnt = 1; } break;
+        }
+        if (rc == EV_ERROR) continue;
+        eol_generated += (uint64_t)cnt;
+        for (int j = 0; j < cnt; j++) { uint64_t k; fp_put(&out[j], (int64_t)p, a, &k); }
+      }
+    }
+    eol_distinct = n_states;
+  }
+
   clock_gettime(CLOCK_MONOTONIC, &t1);
   double secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 
   printf("{\"result\": \"%s\", \"generated\": %llu, \"distinct\": %llu, \"init\": %llu, \"depth\": %d, \"seconds\": %.6f",
-         RESULT_NAME[result], (unsigned long long)generated, (unsigned long long)n_states,
+         RESULT_NAME[result], (unsigned long long)generated, (unsigned long long)tlc_distinct,
          (unsigned long long)n_init, nlevels, secs);
   /* states left on queue: at an error, TLC's queue when it stopped */
-  printf(", \"left_on_queue\": %llu", (unsigned long long)(result == R_OK ? 0 : n_states - dequeued));
+  printf(", \"left_on_queue\": %llu", (unsigned long long)(result == R_OK ? 0 : tlc_distinct - dequeued));
   if (result == R_OK) {
     printf(", \"outdegree\": [");
     for (int i = 0; i <= max_outdeg && n_states; i++) printf("%s%llu", i ? ", " : "", (unsigned long long)outdeg[i]);
@@ -689,6 +754,8 @@ int main(int argc, char **argv) {
     printf("]");
   }
   if (result != R_OK) {
+    printf(", \"eol_generated\": %llu, \"eol_distinct\": %llu", (unsigned long long)eol_generated,
+           (unsigned long long)eol_distinct);
     if (bad_inv >= 0) printf(", \"invariant\": \"%s\"", INV_NAME[bad_inv]);
     if (result == R_ACTION_ERROR) printf(", \"action\": \"%s\", \"error\": \"%s\"", ACTION_NAME[bad_action], g_errmsg);
     if (result == R_INV_ERROR) printf(", \"error\": \"%s\"", g_errmsg);

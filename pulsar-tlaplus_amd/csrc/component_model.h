@@ -16,7 +16,8 @@
 //      - the messages conjunct of TypeSafe           (:238);
 //      - for CompactionHorizonCorrectness (:259-274), per position i, which
 //        ledger positions witness it: key(p) = key(i) /\ p >= i (an entry's
-//        id is its position), or p = i for a retained null key;
+//        id is its position; the ELSE branch, :272-274, a retained null key
+//        included), and which positions are skipped (null key, not retained);
 //      - the null-key positions DuplicateNullKeyMessage (:280-294) reads.
 //
 // The results are exactly model.h's on the word msgs | k << led_sh (same
@@ -33,7 +34,7 @@ typedef uint32_t lkey;  // local key
 
 struct CompMsgs {
   u64 cm;             // CompactMessages for r = 1..N: N bits at (r - 1) * N
-  u64 need;           // horizon witnesses of position i = 1..N: N bits at (i - 1) * N
+  u64 need;           // horizon witnesses of position i = 1..N: N bits at (i - 1) * N (a position p >= i with key(p) = key(i))
   uint32_t skip;      // positions whose messagesBeforeHorizon entry is Nil (null key, not retained)
   uint32_t null_pos;  // positions 1..Len holding NullKey
   int len;            // Len(messages)
@@ -54,11 +55,12 @@ TLCG_HD CompMsgs comp_msgs_init(const Layout& L, u64 s) {
     const int k = st_key(L, s, i);
     if (i <= c.len && (k >= L.nk || st_val(L, s, i) >= L.nv)) c.msgs_ok = 0;
     c.cm |= compact_mask(L, s, i) << ((i - 1) * L.N);
-    if (k == 0) {
-      if (i <= c.len) c.null_pos |= 1u << (i - 1);
-      if (L.retain) c.need |= (1ull << (i - 1)) << ((i - 1) * L.N);
-      else c.skip |= 1u << (i - 1);
+    if (k == 0 && i <= c.len) c.null_pos |= 1u << (i - 1);
+    if (k == 0 && !L.retain) {
+      c.skip |= 1u << (i - 1);  // messagesBeforeHorizon[i] = Nil
     } else {
+      // the ELSE branch (:272-274), a retained null key included: ledger
+      // positions p >= i holding the same key
       u64 w = 0;
       for (int p = i; p <= L.N; ++p)
         if (st_key(L, s, p) == k) w |= 1ull << (p - 1);
@@ -209,8 +211,8 @@ TLCG_HD int inv_leak_k(const Layout& L, lkey k) {
 TLCG_HD int inv_horizon_k(const Layout& L, const CompMsgs& c, lkey k) {
   const int hz = k_hz(L, k);
   if (hz == 0) return EV_TRUE;
-  const int upto = hz < c.len ? hz : c.len;  // positions with a message
-  const uint32_t live = (uint32_t)nmask(upto) & ~c.skip;
+  if (hz > c.len) return EV_ERROR;  // Len(messagesBeforeHorizon) evaluates messages[len + 1]
+  const uint32_t live = (uint32_t)nmask(hz) & ~c.skip;
   if (live) {
     const int ctx = k_ctx(L, k);
     // the first live position evaluates compactedLedgers[ctx]
@@ -220,7 +222,7 @@ TLCG_HD int inv_horizon_k(const Layout& L, const CompMsgs& c, lkey k) {
     for (int i = 0; i < L.N; ++i) fail |= (uint32_t)((m & ((c.need >> (i * L.N)) & nmask(L.N))) == 0) << i;
     if (fail & live) return EV_FALSE;
   }
-  return hz > c.len ? EV_ERROR : EV_TRUE;  // messages[len + 1] out of domain
+  return EV_TRUE;
 }
 
 // DuplicateNullKeyMessage, compaction.tla:280-294 (model.h inv_dupnull)

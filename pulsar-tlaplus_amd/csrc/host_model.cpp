@@ -425,6 +425,19 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
           (x1 && t2w != (msgs | ((u64)c2 << mb))) || check_invariants(L, s) != check_invariants_k(L, cm, k) ||
           selfloop_count(L, s) != selfloop_count_k(L, cm, k))
         return -(1 + checked);
+      // the invariants also on words off the reachable space: every single
+      // ledger-position bit flipped (ledgers that are not prefix-closed, where
+      // readings of CompactionHorizonCorrectness can differ) and every
+      // compactionHorizon value
+      for (int j1 = 1; j1 <= L.C; ++j1)
+        for (int p = 0; p <= L.N; ++p) {
+          const u64 v = s ^ (1ull << (led_base(L, j1) + p));
+          if (check_invariants(L, v) != check_invariants_k(L, cm, (lkey)(v >> mb))) return -(1 + checked);
+        }
+      for (u64 h = 0; h < (1ull << L.hz_w); ++h) {
+        const u64 v = fset(s, L.hz_sh, L.hz_w, h);
+        if (check_invariants(L, v) != check_invariants_k(L, cm, (lkey)(v >> mb))) return -(1 + checked);
+      }
       ++checked;
       u64 succ[64];
       const int nsucc = host_successors(L, s, succ, nullptr, 64);

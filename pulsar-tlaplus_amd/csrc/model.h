@@ -374,27 +374,29 @@ TLCG_HD int inv_leak(const Layout& L, W s) {
   return popcount<W>(s & present_mask<W>(L)) <= 2 ? EV_TRUE : EV_FALSE;
 }
 
-// CompactionHorizonCorrectness, compaction.tla:259-274.  The LET-bound
-// compactedLedgers[compactedTopicContext] is only evaluated (and can only
-// fail) for an i that reaches it, in TLC's left-to-right order.
+// CompactionHorizonCorrectness, compaction.tla:259-274, read literally.
+// Len(messagesBeforeHorizon) (:269) enumerates the function, so messages[i]
+// is evaluated for every i <= compactionHorizon before any i is tested: an i
+// past Len(messages) is an evaluation error first ([TLC-ext]).
+// messagesBeforeHorizon[i] is Nil only for a null key without RetainNullKey
+// (:263-266), and then `RetainNullKey => ...` (:271) holds unevaluated; every
+// other message, a retained null-key one included, takes the ELSE branch
+// (:272-274): some ledger entry with the same key and id >= i (an entry's id
+// is its position).  The LET-bound compactedLedgers[compactedTopicContext] is
+// evaluated (and can fail) only for an i that reaches it, left to right.
 template <typename W>
 TLCG_HD int inv_horizon(const Layout& L, W s) {
   int hz = st_hz(L, s), len = st_len(L, s), ctx = st_ctx(L, s);
+  if (hz > len) return EV_ERROR;  // messages[len + 1] out of domain
   for (int i = 1; i <= hz; ++i) {
-    if (i > len) return EV_ERROR;  // messages[i] out of domain
     int k = st_key(L, s, i);
     if (k == 0 && !L.retain) continue;  // messagesBeforeHorizon[i] = Nil
     if (ctx < 1 || ctx > L.C || !led_present(L, s, ctx)) return EV_ERROR;
     u64 m = led_mask(L, s, ctx);
-    int found;
-    if (k == 0) {
-      found = (int)((m >> (i - 1)) & 1);  // the same record must be in the ledger
-    } else {
-      found = 0;  // \E entry: entry.key = key /\ entry.id >= i
-      u64 rest = m >> (i - 1);
-      for (int p = i; rest && !found; ++p, rest >>= 1)
-        if ((rest & 1) && st_key(L, s, p) == k) found = 1;
-    }
+    int found = 0;  // \E j: compactedLedger[j].key = key /\ compactedLedger[j].id >= i
+    u64 rest = m >> (i - 1);
+    for (int p = i; rest && !found; ++p, rest >>= 1)
+      if ((rest & 1) && st_key(L, s, p) == k) found = 1;
     if (!found) return EV_FALSE;
   }
   return EV_TRUE;

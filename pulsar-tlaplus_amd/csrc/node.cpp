@@ -98,42 +98,47 @@ extern "C" int tlcg_run_node(const tlcg_model* m, const tlcg_opts* base, int32_t
         return fail(first_bad(rc), "tlcg_absorb/tlcg_end_level", c);
     }
   }
-  // combine: counts sum, device times max, the first error's verdict and depth
+  // combine: device times max; the first error -- the one in the lowest level,
+  // then the lowest rank -- gives the verdict and the depth.  A closed
+  // partition's ranks run on independently past another rank's error, so the
+  // counts are cut at the end of the error's level on every rank (levels
+  // 0..E complete, levels 0..E-1 expanded), as one context's level loop stops.
   tlcg_stats out = sts[0];
   out.generated = out.distinct = out.frontier = out.levels_redone = out.host_states = out.fpset_host_states = 0;
   out.kernel_ms = out.expand_ms = 0;
   int first = -1;
   for (int r = 0; r < n; ++r) {
     const tlcg_stats& s = sts[(size_t)r];
-    out.generated += s.generated;
-    out.distinct += s.distinct;
-    out.frontier += s.frontier;
     out.levels_redone += s.levels_redone;
     out.host_states += s.host_states;
     out.fpset_host_states += s.fpset_host_states;
     out.kernel_ms = std::max(out.kernel_ms, s.kernel_ms);
     out.expand_ms = std::max(out.expand_ms, s.expand_ms);
-    // the first error is the one in the lowest level (a closed partition's
-    // ranks run on independently past another rank's error), then lowest rank
     if (s.status != TLCG_DONE && s.status != TLCG_RUNNING && (first < 0 || s.depth < sts[(size_t)first].depth))
       first = r;
   }
+  const size_t cut = first < 0 ? ~(size_t)0 : (size_t)sts[(size_t)first].depth;  // levels kept
+  std::vector<uint64_t> levels, mine(1 << 12), gen(1 << 12);
+  for (int r = 0; r < n; ++r) {
+    int32_t k = 0, kg = 0;
+    if (tlcg_level_sizes(ctxs[(size_t)r], mine.data(), (int32_t)mine.size(), &k) != 0)
+      return fail(r, "tlcg_level_sizes", -1);
+    if (tlcg_level_generated(ctxs[(size_t)r], gen.data(), (int32_t)gen.size(), &kg) != 0)
+      return fail(r, "tlcg_level_generated", -1);
+    k = std::min<int32_t>(k, (int32_t)mine.size());
+    kg = std::min<int32_t>(kg, (int32_t)gen.size());
+    const size_t kk = std::min<size_t>((size_t)k, cut);
+    if (kk > levels.size()) levels.resize(kk, 0);
+    for (size_t i = 0; i < kk; ++i) levels[i] += mine[i];
+    for (size_t i = 0; i < std::min<size_t>((size_t)kg, cut); ++i) out.generated += gen[i];
+  }
+  while (!levels.empty() && !levels.back()) levels.pop_back();
+  for (uint64_t x : levels) out.distinct += x;
+  out.frontier = first < 0 || levels.empty() ? 0 : levels.back();
   out.status = first < 0 ? TLCG_DONE : sts[(size_t)first].status;
   out.invariant = first < 0 ? -1 : sts[(size_t)first].invariant;
   out.action = first < 0 ? -1 : sts[(size_t)first].action;
   out.event_gidx = first < 0 ? ~0ull : sts[(size_t)first].event_gidx;
-  // per-level sizes summed over ranks (partitioned ranks keep empty levels,
-  // so trailing empty ones are dropped); depth = their number
-  std::vector<uint64_t> levels, mine(1 << 12);
-  for (int r = 0; r < n; ++r) {
-    int32_t k = 0;
-    if (tlcg_level_sizes(ctxs[(size_t)r], mine.data(), (int32_t)mine.size(), &k) != 0)
-      return fail(r, "tlcg_level_sizes", -1);
-    k = std::min<int32_t>(k, (int32_t)mine.size());
-    if ((size_t)k > levels.size()) levels.resize((size_t)k, 0);
-    for (int32_t i = 0; i < k; ++i) levels[(size_t)i] += mine[(size_t)i];
-  }
-  while (!levels.empty() && !levels.back()) levels.pop_back();
   out.depth = first < 0 ? (int32_t)levels.size() : sts[(size_t)first].depth;
   const double d = (double)out.distinct, g = (double)out.generated;
   out.fp_collision_optimistic = d * (g - d) / 18446744073709551616.0;

@@ -692,8 +692,10 @@ struct tlcg_ctx {
   };
   std::vector<CompPass> passes;
   std::vector<u64> comp_levels;
+  std::vector<u64> comp_level_gen;  // successors generated by expanding each level
+  u64 comp_init = 0;                // initial states of this rank
   u64 comp_generated = 0, comp_distinct = 0, comp_store_used = 0;
-  unsigned long long* d_comp = nullptr;  // lvl[COMP_MAXLV], totals[2], event, ovf_n
+  unsigned long long* d_comp = nullptr;  // lvl[COMP_MAXLV], totals[2], event, ovf_n, outdeg[3], lvl_gen[COMP_MAXLV]
   unsigned long long* h_comp = nullptr;
   u64* d_ovf[2] = {nullptr, nullptr};
   u64 ovf_cap = 0;
@@ -1574,6 +1576,9 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
 
 // ---- component engine (component.h) ----
 
+// device counters of a component pass (d_comp / h_comp)
+constexpr int kCompCounters = 2 * COMP_MAXLV + 7;
+
 // applicable: `messages` immutable, one rank's components all local, local key fits 32 bits,
 // N <= 8 (component_model.h packs N x N bit masks)
 bool component_applicable(const tlcg_ctx* c) {
@@ -1585,7 +1590,7 @@ bool component_applicable(const tlcg_ctx* c) {
 
 bool comp_scratch(tlcg_ctx* c, u64 n) {
   if (!c->d_comp) {
-    const size_t bytes = sizeof(unsigned long long) * (COMP_MAXLV + 7);
+    const size_t bytes = sizeof(unsigned long long) * kCompCounters;
     if (!alloc_bytes(c, (void**)&c->d_comp, bytes, "component counters")) return false;
     HIPCHK(hipHostMalloc((void**)&c->h_comp, bytes));
   }
@@ -1613,6 +1618,8 @@ int run_component(tlcg_ctx* c) {
   c->engine = TLCG_ENGINE_COMPONENT;
   c->passes.clear();
   c->comp_levels.assign(COMP_MAXLV, 0);
+  c->comp_level_gen.assign(COMP_MAXLV, 0);
+  c->comp_init = r1 - r0;
   c->comp_generated = c->comp_distinct = c->comp_store_used = 0;
   c->outdeg.assign(3, 0);
   c->outdeg_valid = c->opts.outdegree;  // the component engine's parents are TLC's first discoverers
@@ -1648,7 +1655,7 @@ int run_component(tlcg_ctx* c) {
       HIPCHK_I(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
     }
     const int out = cur == 0 ? 1 : 0;
-    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * (COMP_MAXLV + 7), c->stream));
+    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * kCompCounters, c->stream));
     HIPCHK_I(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
     CompArgs a;
     a.L = L;
@@ -1665,6 +1672,7 @@ int run_component(tlcg_ctx* c) {
     a.event = c->d_comp + COMP_MAXLV + 2;
     a.ovf_n = c->d_comp + COMP_MAXLV + 3;
     a.outdeg = c->opts.outdegree ? c->d_comp + COMP_MAXLV + 4 : nullptr;
+    a.lvl_gen = c->d_comp + COMP_MAXLV + 7;
     a.ovf_list = c->d_ovf[out];
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
     if (!(c->jit_used ? jit_launch_component(c->jit, a, K, c->stream) : launch_component(a, K, c->stream))) {
@@ -1672,14 +1680,17 @@ int run_component(tlcg_ctx* c) {
       return -1;
     }
     HIPCHK_I(hipEventRecord(c->e1, c->stream));
-    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * (COMP_MAXLV + 7),
+    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * kCompCounters,
                           hipMemcpyDeviceToHost, c->stream));
     HIPCHK_I(hipStreamSynchronize(c->stream));
     float ms = 0;
     hipEventElapsedTime(&ms, c->e0, c->e1);
     c->kernel_ms += ms;
     c->expand_ms += ms;
-    for (int l = 0; l < COMP_MAXLV; ++l) c->comp_levels[(size_t)l] += c->h_comp[l];
+    for (int l = 0; l < COMP_MAXLV; ++l) {
+      c->comp_levels[(size_t)l] += c->h_comp[l];
+      c->comp_level_gen[(size_t)l] += c->h_comp[COMP_MAXLV + 7 + l];
+    }
     c->comp_generated += c->h_comp[COMP_MAXLV];
     for (int i = 0; i < 3; ++i) c->outdeg[(size_t)i] += c->h_comp[COMP_MAXLV + 4 + i];
     c->comp_distinct += c->h_comp[COMP_MAXLV + 1];
@@ -1693,12 +1704,17 @@ int run_component(tlcg_ctx* c) {
   while (!c->comp_levels.empty() && c->comp_levels.back() == 0) c->comp_levels.pop_back();
   if (best_ev != NO_EVENT) {
     if (!resolve_comp_event(c, best_ev)) return -1;
-    // like the level loop, stop at the end of the level that found the error:
-    // depth and distinct count to there (every lane ran its component out)
+    // like the level loop of the global engine, stop at the end of the level
+    // that found the error: level E = the error's (the violating state's, or
+    // the one after the failing / deadlocked state's) is complete, levels
+    // 0..E-1 are expanded.  Lanes that found an error finished expanding their
+    // level; the others ran their components out, so levels past E are cut.
     const size_t lv = (size_t)(best_ev >> 56) + 1;
     if (c->comp_levels.size() > lv) c->comp_levels.resize(lv);
     c->comp_distinct = 0;
     for (u64 x : c->comp_levels) c->comp_distinct += x;
+    c->comp_generated = c->comp_init;  // initial states count as generated
+    for (size_t l = 0; l + 1 < lv && l < c->comp_level_gen.size(); ++l) c->comp_generated += c->comp_level_gen[l];
     return 1;
   }
   c->status = TLCG_DONE;
@@ -2360,6 +2376,42 @@ int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, ui
   return 0;
 }
 
+// States generated per level (tlcgpu.h): out[0] = initial states, out[k] =
+// successors generated by expanding level k - 1.
+int tlcg_level_generated(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
+  if (!c || !n) return -1;
+  std::vector<u64> v;
+  if (c->engine == TLCG_ENGINE_COMPONENT) {
+    if (c->comp_levels.empty()) {
+      *n = 0;
+      return 0;
+    }
+    v.push_back(c->comp_init);
+    // expanded levels: all of them on a complete run; 0..E-1 at an error in level E
+    const size_t expanded = c->status == TLCG_DONE ? c->comp_levels.size() : c->comp_levels.size() - 1;
+    for (size_t l = 0; l < expanded && l < c->comp_level_gen.size(); ++l) v.push_back(c->comp_level_gen[l]);
+  } else {
+    if (c->level_base.size() < 2) {
+      *n = 0;
+      return 0;
+    }
+    if (c->gen_at.size() + 2 < c->level_base.size()) {
+      c->err = "per-level generated counts are not available for a recovered run";
+      return -2;
+    }
+    if (c->gen_at.empty()) {
+      v.push_back(c->generated);
+    } else {
+      v.push_back(c->gen_at[0]);
+      for (size_t k = 1; k < c->gen_at.size(); ++k) v.push_back(c->gen_at[k] - c->gen_at[k - 1]);
+      v.push_back(c->generated - c->gen_at.back());
+    }
+  }
+  *n = (int32_t)v.size();
+  for (size_t i = 0; i < v.size() && (int32_t)i < cap; ++i) out[i] = v[i];
+  return 0;
+}
+
 // TLC's outdegree histogram of a completed check (tlcgpu.h)
 int tlcg_outdegree(tlcg_ctx* c, uint64_t* hist, int32_t cap, int32_t* n) {
   if (!c || !n) return -1;
@@ -2520,10 +2572,26 @@ int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
     c->err = "the checkpoint was taken for other constants or options";
     return -4;
   }
-  std::vector<u64> lb(h.n_levels);
-  if (std::fread(lb.data(), 8, lb.size(), f) != lb.size() || lb.back() != h.distinct) {
+  // the header's sizes must match the file before anything is sized from
+  // them: level bases (8 B each), then states (8 B x words) and parent refs
+  // (8 B) of every distinct state
+  const long body = std::ftell(f);
+  std::fseek(f, 0, SEEK_END);
+  const long fsize = std::ftell(f);
+  std::fseek(f, body, SEEK_SET);
+  const u64 avail = body >= 0 && fsize > body ? (u64)(fsize - body) : 0;
+  const u64 per_state = 8 * (u64)c->words + 8;
+  if (h.n_levels > avail / 8 || h.distinct > avail / per_state || h.n_levels * 8 + h.distinct * per_state != avail) {
     std::fclose(f);
-    c->err = "checkpoint file is truncated";
+    c->err = "checkpoint file is truncated or corrupt (its sizes do not match the file)";
+    return -3;
+  }
+  std::vector<u64> lb(h.n_levels);
+  bool lb_ok = std::fread(lb.data(), 8, lb.size(), f) == lb.size() && lb[0] == 0 && lb.back() == h.distinct;
+  for (size_t i = 1; lb_ok && i < lb.size(); ++i) lb_ok = lb[i] >= lb[i - 1];
+  if (!lb_ok) {
+    std::fclose(f);
+    c->err = "checkpoint file is truncated or corrupt (level bases)";
     return -3;
   }
   // the run restarts on the global engine with exactly the committed levels
@@ -2689,6 +2757,8 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
     if ((ovf & OVF_STORE) && !ensure_store(c, d + std::max<u64>(c->h_ctr->n_new, 2 * dev_room(c, d)))) return -10;
     if (!regrow_fpset(c, ovf, d)) return -10;
   }
+  c->gen_at.resize((size_t)depth - 1);
+  c->gen_at.push_back(c->generated);
   c->generated += c->h_ctr->generated;
   c->pending = c->h_ctr->n_new;
   fill_stats(c, st);

@@ -302,12 +302,34 @@ int main(int argc, char** argv) {
       to.tlc_order = 1;
       to.engine = TLCG_ENGINE_GLOBAL;
       if (!ctx) to.device = 0;
+      // the first run's device memory is released before the re-run, which
+      // needs as much again (and more: TLC order keeps discovery keys)
+      tlcg_destroy(ctx);
+      ctx = nullptr;
+      tctx = nullptr;
+      std::string why;
       if (tlcg_create(&model, &to, &tctx) == 0 && tlcg_run(tctx, &tst) == 0 && tst.status == st.status) {
         own = true;
       } else {
-        if (tctx && tctx != ctx) tlcg_destroy(tctx);
-        tctx = ctx;
+        why = tctx ? tlcg_last_error(tctx) : "tlcg_create failed";
+        tlcg_destroy(tctx);
+        tctx = nullptr;
         tst = st;
+        // fall back to the first run's engine and order: a shortest
+        // counterexample, but not necessarily the one TLC -workers 1 prints
+        tlcg_opts fo = opts;
+        if (!o.recover.empty() || o.gpus > 1) fo.engine = TLCG_ENGINE_GLOBAL;
+        tlcg_stats fst;
+        if (tlcg_create(&model, &fo, &tctx) == 0 && tlcg_run(tctx, &fst) == 0 && fst.status == st.status) {
+          own = true;
+          std::printf("Warning: the TLC-order re-run for the trace failed (%s); the trace below is a shortest "
+                      "counterexample but may not be the one TLC prints, and the counts are at the end of the "
+                      "level.\n", why.c_str());
+        } else {
+          tlcg_destroy(tctx);
+          tctx = nullptr;
+          std::printf("Warning: no trace: the re-run for it failed (%s).\n", why.c_str());
+        }
       }
     }
     switch (tst.status) {

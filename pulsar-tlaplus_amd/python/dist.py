@@ -43,6 +43,8 @@ class DistResult:
     kernel_ms: float
     expand_ms: float
     closed: bool
+    invariant: Optional[int] = None         # index into the model's invariants (first error)
+    first_error_rank: Optional[int] = None
 
 
 class GpuEngine:
@@ -105,6 +107,9 @@ class GpuEngine:
     def level_sizes(self) -> List[int]:
         return self.ck.level_sizes()
 
+    def level_generated(self) -> List[int]:
+        return self.ck.level_generated()
+
     def new_tensor(self, shape, dtype):
         return torch.empty(shape, dtype=dtype, device=f"cuda:{self.device}")
 
@@ -113,28 +118,41 @@ class GpuEngine:
 
 
 def _reduce_result(engine, stats, group, dev: torch.device) -> DistResult:
+    """Combine the ranks' results like one context's level loop would report
+    them.  The first error -- lowest level, then lowest rank (node.cpp does
+    the same) -- gives the verdict and the depth E + 1.  A closed partition's
+    ranks run on independently past another rank's error, so every rank's
+    counts are cut at the end of level E: levels 0..E, and the states
+    generated up to that level (tlcg_level_generated)."""
     levels = engine.level_sizes()
-    depth_local = len(levels)
-    t = torch.tensor([stats.generated, stats.distinct], dtype=torch.int64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    d = torch.tensor([depth_local], dtype=torch.int64, device=dev)
-    dist.all_reduce(d, op=dist.ReduceOp.MAX, group=group)
-    depth = int(d.item())
-    lv = torch.zeros(max(depth, 1), dtype=torch.int64, device=dev)
-    if levels:
-        lv[: len(levels)] = torch.tensor(levels, dtype=torch.int64, device=dev)
-    dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
-    # the first error in (level, rank) order wins; 0 = no error
+    lgen = engine.level_generated()
+    me = dist.get_rank(group)
     st = int(stats.status)
-    code = torch.tensor([st if st >= 2 else 0], dtype=torch.int64, device=dev)
-    dist.all_reduce(code, op=dist.ReduceOp.MAX, group=group)
-    status = tlcgpu.STATUS[int(code.item())] if code.item() else "ok"
+    none = 1 << 62
+    key = torch.tensor([(len(levels) << 16) | me if st >= 2 else none], dtype=torch.int64, device=dev)
+    dist.all_reduce(key, op=dist.ReduceOp.MIN, group=group)
+    k = int(key.item())
+    first, cut = (None, None) if k == none else (k & 0xFFFF, k >> 16)
+    mine = levels if cut is None else levels[:cut]
+    g = sum(lgen) if cut is None else sum(lgen[:cut])
+    inv = getattr(stats, "invariant", -1)
+    info = torch.tensor([len(mine), g, st if first == me else 0, inv + 1 if first == me else 0],
+                        dtype=torch.int64, device=dev)
+    n = torch.tensor([len(mine)], dtype=torch.int64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    lv = torch.zeros(max(int(n.item()), 1), dtype=torch.int64, device=dev)
+    if mine:
+        lv[: len(mine)] = torch.tensor(mine, dtype=torch.int64, device=dev)
+    dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(info, op=dist.ReduceOp.SUM, group=group)
     levels_all = [int(x) for x in lv.tolist()]
     while levels_all and levels_all[-1] == 0:
         levels_all.pop()
-    return DistResult(status=status, generated=int(t[0].item()), distinct=int(t[1].item()),
-                      depth=len(levels_all), levels=levels_all, kernel_ms=stats.kernel_ms,
-                      expand_ms=stats.expand_ms, closed=engine.closed)
+    code, inv_all = int(info[2].item()), int(info[3].item()) - 1
+    return DistResult(status=tlcgpu.STATUS[code] if first is not None else "ok", generated=int(info[1].item()),
+                      distinct=sum(levels_all), depth=cut if cut is not None else len(levels_all),
+                      levels=levels_all, kernel_ms=stats.kernel_ms, expand_ms=stats.expand_ms, closed=engine.closed,
+                      invariant=inv_all if inv_all >= 0 else None, first_error_rank=first)
 
 
 def _transport_device(group, dev: torch.device) -> torch.device:

@@ -81,6 +81,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_step_level": (C.c_int, [P, S]),
         "tlcg_run": (C.c_int, [P, S]),
         "tlcg_level_sizes": (C.c_int, [P, C.POINTER(U64), I32, C.POINTER(I32)]),
+        "tlcg_level_generated": (C.c_int, [P, C.POINTER(U64), I32, C.POINTER(I32)]),
         "tlcg_trace": (C.c_int, [P, C.POINTER(U64), C.POINTER(I32), I32, C.POINTER(I32)]),
         "tlcg_state_at": (C.c_int, [P, U64, C.POINTER(U64), C.POINTER(U64)]),
         "tlcg_copy_states": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
@@ -346,6 +347,14 @@ class Checker:
         buf = (C.c_uint64 * 65536)()
         n = C.c_int32()
         self._chk(self.lib.tlcg_level_sizes(self.ctx, buf, 65536, C.byref(n)), "tlcg_level_sizes")
+        return [buf[i] for i in range(min(n.value, 65536))]
+
+    def level_generated(self) -> List[int]:
+        """[0] initial states, [k] successors generated by expanding level k - 1
+        (tlcg_level_generated)."""
+        buf = (C.c_uint64 * 65536)()
+        n = C.c_int32()
+        self._chk(self.lib.tlcg_level_generated(self.ctx, buf, 65536, C.byref(n)), "tlcg_level_generated")
         return [buf[i] for i in range(min(n.value, 65536))]
 
     def trace(self) -> List[Tuple[str, int]]:

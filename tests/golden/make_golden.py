@@ -114,6 +114,8 @@ def main():
                 # TLC's counters where the one-worker run stops
                 assert (p["generated"], p["distinct"], p["left_on_queue"]) == \
                        (r["generated"], r["distinct"], r["left_on_queue"]), name
+                # a level-synchronous checker's counts: the level that found the error finished
+                assert (p["eol_generated"], p["eol_distinct"]) == (r["eol_generated"], r["eol_distinct"]), name
         golden[name] = dict(constants=c, result=r)
         print(f"{name:24s} {r['result']:10s} gen={r['generated']} distinct={r.get('distinct')} depth={r.get('depth')}")
     assert golden["S"]["result"]["distinct"] == 45198            # compaction.tla:23

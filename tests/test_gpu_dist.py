@@ -40,19 +40,28 @@ def _worker(rank, world, port, case, partition, outdir):
         eng.close()
         with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
             json.dump(dict(status=r.status, generated=r.generated, distinct=r.distinct, depth=r.depth,
-                           levels=r.levels, closed=r.closed), f)
+                           levels=r.levels, closed=r.closed, invariant=r.invariant), f)
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("case,partition,world", [("S", 2, 2), ("P_published", 0, 2), ("P_published", 0, 3),
-                                                  ("X_keys3_vals57", 2, 3), ("S", 0, 2)])
+                                                  ("X_keys3_vals57", 2, 3), ("S", 0, 2),
+                                                  ("V_leak", 0, 2), ("V_leak", 2, 3), ("V_dup", 0, 3),
+                                                  ("V_dup", 2, 2), ("V_leak_producer", 0, 2)])
 def test_gpu_ranks_match_single(tmp_path, case, partition, world):
     mp.spawn(_worker, args=(world, _free_port(), case, partition, str(tmp_path)), nprocs=world, join=True)
     want = GOLDEN[case]["result"]
+    c = GOLDEN[case]["constants"]
     for rank in range(world):
         r = json.load(open(tmp_path / f"r{rank}.json"))
-        assert r["closed"] == (partition != 2 and not GOLDEN[case]["constants"]["producer"])
+        assert r["closed"] == (partition != 2 and not c["producer"])
         assert r["status"] == want["result"]
-        assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (
-            want["generated"], want["distinct"], want["depth"], want["levels"])
+        if want["result"] == "ok":
+            assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (
+                want["generated"], want["distinct"], want["depth"], want["levels"])
+        else:  # the first error (lowest level, then rank); counts at the end of its level
+            assert c["invariants"][r["invariant"]] == want["invariant"]
+            assert (r["generated"], r["distinct"], r["depth"]) == (
+                want["eol_generated"], want["eol_distinct"], want["depth"])
+            assert r["levels"][:-1] == want["levels"][:-1] and sum(r["levels"]) == want["eol_distinct"]

@@ -25,7 +25,10 @@ def check_against_golden(case, r, tlc_order):
         return
     # an error stops the run at the end of the level that found it: the depth
     # and the trace are TLC's; generated/distinct are counted to that level end
+    # (the oracles' eol_* counts), the same for every engine and order
     assert r.depth == want["depth"], (case, r.engine, r.depth)
+    assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"]), (case, r.engine)
+    assert sum(r.levels) == r.distinct, (case, r.engine)
     m = model_of(GOLDEN[case]["constants"])
     want_trace = want["trace"]
     assert len(r.trace) == len(want_trace)

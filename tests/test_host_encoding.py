@@ -119,6 +119,44 @@ def test_component_specialization_matches_generic(case):
     assert n > 0 or (n == 0 and bits > 32), n
 
 
+def test_horizon_correctness_retained_null_key_takes_else_branch():
+    """CompactionHorizonCorrectness (compaction.tla:262-274) read literally:
+    with RetainNullKey = TRUE, messagesBeforeHorizon[i] of a null-key message
+    is the message itself, never Nil, so the ELSE branch applies -- some ledger
+    entry with key 0 and id >= i witnesses it.  A ledger holding message 2 (a
+    null key) but not message 1 (also a null key) therefore satisfies i = 1.
+    "The same record must be in the ledger" would say FALSE here; the two
+    readings differ only off the reachable space (reachable ledgers keep every
+    null-key message up to their read position)."""
+    import oracle_py
+    m = tlcgpu.Model()  # S: RetainNullKey = TRUE, invariants TypeSafe, CompactionHorizonCorrectness
+    s = tlcgpu.host_init_state(m, 81)  # <<(1, key 0), (2, key 0), (3, key 1)>>
+    for _ in range(4):  # PhaseOne, Write, UpdateContext, UpdateHorizon: hz = 3, ctx = 1
+        s = [t for a, t in tlcgpu.host_successors(m, s) if a != "BrokerCrash"][0]
+    assert tlcgpu.host_check_invariants(m, s) == -1
+    full = "<<<<[id |-> 1, key |-> 0, value |-> 0], [id |-> 2, key |-> 0, value |-> 0], [id |-> 3, key |-> 1, value |-> 0]>>, Nil, Nil>>"
+    want = "<<<<[id |-> 2, key |-> 0, value |-> 0], [id |-> 3, key |-> 1, value |-> 0]>>, Nil, Nil>>"
+    assert full in tlcgpu.decode(m, s)
+    # the word whose ledger 1 lacks message 1: one flipped bit of the packed state
+    v, = [s ^ (1 << b) for b in range(tlcgpu.state_bits(m)) if want in tlcgpu.decode(m, s ^ (1 << b))]
+    assert "compactionHorizon = 3" in tlcgpu.decode(m, v) and "compactedTopicContext = 1" in tlcgpu.decode(m, v)
+    assert tlcgpu.host_check_invariants(m, v) == -1  # the ELSE branch holds for i = 1 (entry 2: key 0, id 2 >= 1)
+    # the Python oracle on the same TLC values
+    py = oracle_py.Model(N=3, C=3, K=1, keys=[1, 2], values=[1, 2], retain=True, producer=False, consumer=False, ctl=2)
+    msgs = ((1, 0, 0), (2, 0, 0), (3, 1, 0))
+    state = (msgs, (msgs[1:], None, None), None, oracle_py.W + 3, None, 3, 1, 0, 0)
+    assert py.inv("CompactionHorizonCorrectness", state) is True
+    # drop message 2 as well: no entry with key 0 remains, i = 1 fails
+    state = (msgs, (msgs[2:], None, None), None, oracle_py.W + 3, None, 3, 1, 0, 0)
+    assert py.inv("CompactionHorizonCorrectness", state) is False
+    w = v ^ next(1 << b for b in range(tlcgpu.state_bits(m))
+                 if "<<<<[id |-> 3, key |-> 1, value |-> 0]>>, Nil, Nil>>" in tlcgpu.decode(m, v ^ (1 << b)))
+    assert tlcgpu.host_check_invariants(m, w) == (1 << 1)  # index 1 (CompactionHorizonCorrectness), false
+    # the component engine's specialized evaluators agree on such words too
+    # (tlcg_host_component_selfcheck flips every ledger bit of every state)
+    assert tlcgpu.host_component_selfcheck(m, 81, 1) > 0
+
+
 @pytest.mark.parametrize("case", ["S", "P_published", "S_consumer", "W_C12_k1", "D_N0_K0", "X_empty_spaces"])
 def test_termination_counterexample(case):
     """PROPERTY Termination: Spec has no fairness, so <>P fails iff an initial
