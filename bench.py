@@ -179,6 +179,8 @@ def main():
     import torch
     import tlcgpu
 
+    # a collective that does not complete (a peer rank died) aborts instead of hanging
+    os.environ.setdefault("TLCG_COMM_TIMEOUT_S", "180")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -243,43 +245,44 @@ def main():
 
     def time_exchange(partition):
         """The global engine with successors crossing ranks, so every BFS level
-        runs expand -> all-to-all of {state, parent} records (RCCL over xGMI) ->
-        absorb -> all-reduce (dist.run).  BASELINE config 4: on G9 the FPSet is
-        partitioned on the whole state (partition 2); a producer-modelled cfg
-        is open by itself (partition 0)."""
+        runs expand -> all-gather of counts -> send/recv of {state, parent}
+        records over RCCL (xGMI) -> absorb -> all-reduce, all inside libtlcgpu
+        (tlcg_run_comm; dist.run_native).  BASELINE config 4: on G9 the FPSet
+        is partitioned on the whole state (partition 2); a producer-modelled
+        cfg is open by itself (partition 0)."""
         per_rank = cfg["distinct"] // world + 1
         log2 = max(16, (2 * per_rank - 1).bit_length())
         cap = int(per_rank * 1.1) + (1 << 20)
         eng = tdist.GpuEngine(model, rank, world, gpu, log2_fpset_slots=log2, state_capacity=cap, engine="global",
                               partition=partition)
         assert not eng.closed
+        tdist.init_native(eng)
         for _ in range(args.warmup):
-            tdist.run(eng, dev=rdev)
+            tdist.run_native(eng)
         torch.cuda.synchronize(dev)
         dist.barrier()
         torch.cuda.synchronize(dev)
-        timing = {}
         kms = ems = 0.0
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            r = tdist.run(eng, dev=rdev, timing=timing)
+            r = tdist.run_native(eng)
             kms += r.kernel_ms
             ems += r.expand_ms
         torch.cuda.synchronize(dev)
         dist.barrier()
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
-        t = torch.tensor([elapsed, timing.get("exchange_s", 0.0), ems, kms], dtype=torch.float64, device=rdev)
+        t = torch.tensor([elapsed, ems, kms], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         eng.close()
         if (r.generated, r.distinct, r.depth) != (cfg["generated"], cfg["distinct"], cfg["depth"]):
             raise SystemExit(f"count mismatch (exchange): {(r.generated, r.distinct, r.depth)} want {cfg}")
-        return dict(engine="global", jit=0, elapsed=float(t[0]), expand_ms=float(t[2]) / args.steps,
-                    kernel_ms=float(t[3]) / args.steps, launches=cfg["depth"] - 1,
+        return dict(engine="global", jit=0, elapsed=float(t[0]), expand_ms=float(t[1]) / args.steps,
+                    kernel_ms=float(t[2]) / args.steps, launches=cfg["depth"] - 1,
                     kernel="k_expand<u64, open partition> + k_absorb",
                     partition="whole state (owner = mix64(state))" if partition == 2 else "open (Producer)",
-                    exchange="all_to_all_single per level, " + dist.get_backend(),
-                    exchange_ms_per_step=round(float(t[1]) * 1e3 / args.steps, 3))
+                    exchange="libtlcgpu tlcg_run_comm: ncclAllGather (counts) + grouped ncclSend/ncclRecv "
+                             "(16-B records) + ncclAllReduce per level, RCCL over xGMI")
 
     open_model = bool(cfg.get("producer"))
     exchange_run = global_run = None
@@ -373,7 +376,7 @@ def main():
                    ms_per_step=round(r["elapsed"] * 1e3 / args.steps, 3),
                    gpu_kernel_ms_per_step=round(r["kernel_ms"], 3),
                    roofline=roofline_component(r) if r["engine"] == "component" else roofline_global(r))
-        for k in ("partition", "exchange", "exchange_ms_per_step"):
+        for k in ("partition", "exchange"):
             if k in r:
                 out[k] = r[k]
         return out

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TLCG_ABI_VERSION 1
+#define TLCG_ABI_VERSION 2
 #define TLCG_MAX_SET 63 /* largest KeySpace / ValueSpace */
 #define TLCG_MAX_INV 8
 
@@ -146,6 +146,7 @@ typedef struct tlcg_stats {
   uint64_t jit_used;         /* 1: the layout-specialized (hipRTC) component kernels ran */
   uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
   uint64_t fpset_host_states; /* states held by the host FPSet tier (tlcg_opts.fpset_spill) */
+  uint64_t transport;        /* multi-rank runs: 1 host threads + device copies, 2 RCCL; 0 one context */
 } tlcg_stats;
 
 typedef struct tlcg_ctx tlcg_ctx;
@@ -282,13 +283,34 @@ int tlcg_exchange_local(tlcg_ctx* const* ctxs, int32_t n, uint64_t* n_in);
 int tlcg_partition_closed(const tlcg_ctx* c);
 /* The whole check by one process on the node's GPUs (tlc-hip -gpus N): n
  * ranks, rank r on device r mod tlcg_device_count(), each driven from its own
- * host thread; a closed partition runs each rank to completion, an open one
- * runs expand -> tlcg_exchange_local -> absorb per level.  *st gets the
- * combined verdict (counts summed, the lowest failing rank's error, depth from
- * the summed level sizes, which go to levels[0..cap) and *n_levels).  The
+ * host thread through the level loop of tlcg_run_comm.  The records move over
+ * RCCL (ncclCommInitAll) when every rank has a device of its own, else by
+ * device-to-device copies between threads (TLCG_NODE_TRANSPORT=local|rccl
+ * forces one; st->transport says which ran).  *st gets the combined verdict
+ * (the first error by level then rank, every rank's counts cut at the end of
+ * its level; level sizes summed into levels[0..cap), *n_levels).  The
  * contexts are destroyed before return; a trace is re-derived on one GPU. */
 int tlcg_run_node(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_stats* st, uint64_t* levels,
                   int32_t cap, int32_t* n_levels, char* err, int32_t err_cap);
+
+/* ---- one process per GPU over RCCL (xGMI) ----
+ * Rank 0 calls tlcg_comm_unique_id and hands the 128 bytes to every rank (the
+ * caller's own channel, e.g. a torch.distributed broadcast); every rank
+ * creates its context (tlcg_opts.rank / world) and calls tlcg_comm_init with
+ * them; then tlcg_run_comm runs the whole check on all ranks: a closed
+ * partition runs each rank alone, an open one runs every BFS level as
+ * expand -> ncclAllGather of the per-destination counts -> grouped
+ * ncclSend/ncclRecv of the 16-B records -> absorb, with an ncclAllReduce
+ * deciding termination.  *st and levels[0..*n_levels) are the combined result
+ * (the same on every rank; the first error by level, then rank, with every
+ * rank's counts cut at the end of its level).  A collective that does not
+ * complete within TLCG_COMM_TIMEOUT_S seconds (default 600) aborts the
+ * communicator and returns an error.  RCCL is loaded at run time
+ * (librccl.so.1); tlcg_comm_available says whether it can be. */
+int tlcg_comm_available(void);
+int tlcg_comm_unique_id(void* id, int32_t cap);
+int tlcg_comm_init(tlcg_ctx* c, const void* id, int32_t len);
+int tlcg_run_comm(tlcg_ctx* c, tlcg_stats* st, uint64_t* levels, int32_t cap, int32_t* n_levels);
 
 /* TLC -checkpoint: write the run's committed levels (state store + parent
  * log, level sizes, counters) to `path` between levels of a global-engine

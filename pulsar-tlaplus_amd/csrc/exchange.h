@@ -1,0 +1,67 @@
+// pulsar-tlaplus_amd/csrc/exchange.h -- the multi-rank BFS level loop and the
+// transports that move its data between ranks (internal to libtlcgpu.so).
+//
+// One rank = one tlcg_ctx owning a shard of the fingerprint space (SURVEY
+// 8(e); TLC's distributed FPSetManager).  run_ranks() is the whole check of
+// one rank: a closed partition (no action writes `messages`) runs alone and
+// only the results are combined; an open one runs, per BFS level,
+//   tlcg_expand -> counts (all-gather) -> records (grouped send/recv of the
+//   16-B {state, parent_ref} outboxes) -> tlcg_absorb -> tlcg_end_level,
+// with a small all-reduce deciding termination.  Two transports carry it:
+//   RcclTransport  -- RCCL over xGMI (one communicator per rank, on the
+//                     context's stream; one process per GPU or one thread
+//                     per GPU);
+//   LocalTransport -- host threads of one process sharing a board, records
+//                     copied device to device (ranks that share a GPU).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "tlcgpu.h"
+
+namespace tlcg {
+
+enum RedOp { RED_SUM = 0, RED_MIN = 1, RED_MAX = 2 };
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  // row[d] = records this rank holds for rank d (row[rank] = 0), row[world] =
+  // this rank's failure flag; out gets every rank's row (world x (world + 1))
+  virtual bool allgather_rows(const uint64_t* row, uint64_t* out, std::string* err) = 0;
+  // every outbox of ctx to its owner; the inbox (already sized for the sum of
+  // recv) receives them source-rank-major.  Ordered before later work on the
+  // context's stream.
+  virtual bool records(tlcg_ctx* c, const uint64_t* send, const uint64_t* recv, std::string* err) = 0;
+  virtual bool allreduce(uint64_t* v, int n, RedOp op, std::string* err) = 0;
+};
+
+// The check of one rank; *st, levels and the return value are the combined
+// result of all ranks (the same on every rank).  0 ok, < 0 error (err).
+int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* levels, std::string* err);
+
+// RCCL (loaded at run time from librccl.so.1, the ROCm collective library).
+bool rccl_available(std::string* err);
+// a communicator for c (rank and world from its options) from a 128-byte id
+int comm_init(tlcg_ctx* c, const void* id, std::string* err);
+// one communicator per context, all devices distinct, one process (ncclCommInitAll)
+int comm_init_all(tlcg_ctx* const* ctxs, int n, std::string* err);
+Transport* comm_transport(tlcg_ctx* c);  // the context's RCCL transport, or null
+void comm_free(void* comm_state);
+
+// context internals exchange.cpp needs (tlcgpu.hip)
+int ctx_device(const tlcg_ctx* c);
+void ctx_rank_world(const tlcg_ctx* c, int* rank, int* world);
+void*& ctx_comm(tlcg_ctx* c);
+void ctx_set_error(tlcg_ctx* c, const std::string& e);
+
+// The local transport of n ranks driven by n threads of this process.
+struct LocalBoard;
+LocalBoard* local_board_new(tlcg_ctx* const* ctxs, int n);
+void local_board_free(LocalBoard* b);
+Transport* local_transport(LocalBoard* b, int rank);  // owned by the board
+
+}  // namespace tlcg

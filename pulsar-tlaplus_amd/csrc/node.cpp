@@ -1,40 +1,34 @@
 // pulsar-tlaplus_amd/csrc/node.cpp -- tlcg_run_node: one process checks the
 // model on every GPU of a node, one context (rank) per device, the FPSet
-// hash-partitioned by owner.  This is the single-process form of TLC's
-// distributed FPSetManager (tlc2.tool.fp) that `tlc-hip -gpus N` runs; the
-// one-process-per-GPU form over RCCL is python/dist.py.  It uses only the
-// C-ABI of include/tlcgpu.h: every call makes its context's device current,
-// so each rank is driven from its own host thread.
+// hash-partitioned by owner, each rank driven by its own host thread.  This is
+// what `tlc-hip -gpus N` runs; the one-process-per-GPU form is tlcg_comm_init +
+// tlcg_run_comm (python/dist.py run_native).  Both run the same level loop,
+// exchange.cpp run_ranks():
 //
 //   closed partition (no Producer: `messages` is immutable, so successors never
 //     leave their rank, compaction.tla:87,100,132,139,145,151,165,182,186,214):
-//     every rank runs tlcg_run to completion, then the counts are combined;
+//     every rank runs tlcg_run to completion, then the results are combined;
 //   open partition (Producer, or tlcg_opts.partition = 2): every level is
-//     tlcg_expand on all ranks -> tlcg_exchange_local (device-to-device copies
-//     of the {state, parent} records to their owners over xGMI) ->
+//     tlcg_expand -> counts all-gather -> records send/recv to their owners ->
 //     tlcg_absorb + tlcg_end_level, until a rank stops or no rank found a new
 //     state.
+//
+// Transport: RCCL over xGMI (ncclCommInitAll, one communicator per device)
+// when every rank has a device of its own; otherwise (more ranks than
+// devices) host threads meeting at a board, records copied device to device.
+// TLCG_NODE_TRANSPORT=local|rccl forces one.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "exchange.h"
 #include "tlcgpu.h"
 
 namespace {
-
-// f(r) for every rank on its own host thread; the first nonzero result (or 0)
-template <class F>
-int on_all(int n, F f) {
-  std::vector<int> rc((size_t)n, 0);
-  std::vector<std::thread> th;
-  for (int r = 0; r < n; ++r) th.emplace_back([&, r] { rc[(size_t)r] = f(r); });
-  for (auto& t : th) t.join();
-  for (int r = 0; r < n; ++r)
-    if (rc[(size_t)r]) return rc[(size_t)r];
-  return 0;
-}
 
 void put_err(char* err, int32_t cap, const std::string& s) {
   if (err && cap > 0) std::snprintf(err, (size_t)cap, "%s", s.c_str());
@@ -50,22 +44,8 @@ extern "C" int tlcg_run_node(const tlcg_model* m, const tlcg_opts* base, int32_t
   }
   const int ndev = std::max(1, tlcg_device_count());
   std::vector<tlcg_ctx*> ctxs((size_t)n, nullptr);
-  std::vector<tlcg_stats> sts((size_t)n);
-  auto fail = [&](int r, const char* what, int code) {
-    put_err(err, err_cap, std::string(what) + " (rank " + std::to_string(r) + "): " +
-                              (ctxs[(size_t)r] ? tlcg_last_error(ctxs[(size_t)r]) : "no context"));
+  auto destroy_all = [&] {
     for (auto* c : ctxs) tlcg_destroy(c);
-    return code < 0 ? code : -1;
-  };
-  // the first rank whose call failed (its context holds the message)
-  auto first_bad = [&](const std::vector<int>& rc) {
-    for (int r = 0; r < n; ++r)
-      if (rc[(size_t)r]) return r;
-    return 0;
-  };
-  std::vector<int> rc((size_t)n, 0);
-  auto all = [&](auto f) {
-    return on_all(n, [&](int r) { return rc[(size_t)r] = f(r); });
   };
   tlcg_peer_access(std::min(n, ndev));
   for (int r = 0; r < n; ++r) {
@@ -74,78 +54,48 @@ extern "C" int tlcg_run_node(const tlcg_model* m, const tlcg_opts* base, int32_t
     o.rank = r;
     o.world = n;
     const int c = tlcg_create(m, &o, &ctxs[(size_t)r]);
-    if (c) return fail(r, "tlcg_create", c);
-  }
-  if (tlcg_partition_closed(ctxs[0]) == 1) {
-    if (int c = all([&](int r) { return tlcg_run(ctxs[(size_t)r], &sts[(size_t)r]); })) return fail(first_bad(rc), "tlcg_run", c);
-  } else {
-    if (int c = all([&](int r) { return tlcg_init(ctxs[(size_t)r], &sts[(size_t)r]); })) return fail(first_bad(rc), "tlcg_init", c);
-    std::vector<uint64_t> n_in((size_t)n, 0);
-    for (;;) {
-      bool any_new = false, any_stop = false;
-      for (const auto& s : sts) {
-        any_new |= s.frontier > 0;
-        any_stop |= s.status != TLCG_RUNNING;
-      }
-      if (any_stop || !any_new) break;
-      if (int c = all([&](int r) { return tlcg_expand(ctxs[(size_t)r], &sts[(size_t)r]); }))
-        return fail(first_bad(rc), "tlcg_expand", c);
-      if (int c = tlcg_exchange_local(ctxs.data(), n, n_in.data())) return fail(0, "tlcg_exchange_local", c);
-      if (int c = all([&](int r) {
-            const int a = tlcg_absorb(ctxs[(size_t)r], n_in[(size_t)r], &sts[(size_t)r]);
-            return a ? a : tlcg_end_level(ctxs[(size_t)r], &sts[(size_t)r]);
-          }))
-        return fail(first_bad(rc), "tlcg_absorb/tlcg_end_level", c);
+    if (c) {
+      put_err(err, err_cap, "tlcg_create (rank " + std::to_string(r) + "): " +
+                                (ctxs[(size_t)r] ? tlcg_last_error(ctxs[(size_t)r]) : "no context"));
+      destroy_all();
+      return c < 0 ? c : -1;
     }
   }
-  // combine: device times max; the first error -- the one in the lowest level,
-  // then the lowest rank -- gives the verdict and the depth.  A closed
-  // partition's ranks run on independently past another rank's error, so the
-  // counts are cut at the end of the error's level on every rank (levels
-  // 0..E complete, levels 0..E-1 expanded), as one context's level loop stops.
-  tlcg_stats out = sts[0];
-  out.generated = out.distinct = out.frontier = out.levels_redone = out.host_states = out.fpset_host_states = 0;
-  out.kernel_ms = out.expand_ms = 0;
-  int first = -1;
-  for (int r = 0; r < n; ++r) {
-    const tlcg_stats& s = sts[(size_t)r];
-    out.levels_redone += s.levels_redone;
-    out.host_states += s.host_states;
-    out.fpset_host_states += s.fpset_host_states;
-    out.kernel_ms = std::max(out.kernel_ms, s.kernel_ms);
-    out.expand_ms = std::max(out.expand_ms, s.expand_ms);
-    if (s.status != TLCG_DONE && s.status != TLCG_RUNNING && (first < 0 || s.depth < sts[(size_t)first].depth))
-      first = r;
+  const char* force = std::getenv("TLCG_NODE_TRANSPORT");
+  std::string why = n > ndev ? "more ranks than devices" : "TLCG_NODE_TRANSPORT=local";
+  bool rccl = n <= ndev && !(force && !std::strcmp(force, "local")) && tlcg::rccl_available(&why);
+  if (rccl && tlcg::comm_init_all(ctxs.data(), n, &why) != 0) rccl = false;
+  if (!rccl && force && !std::strcmp(force, "rccl")) {
+    put_err(err, err_cap, "TLCG_NODE_TRANSPORT=rccl: " + why);
+    destroy_all();
+    return -30;
   }
-  const size_t cut = first < 0 ? ~(size_t)0 : (size_t)sts[(size_t)first].depth;  // levels kept
-  std::vector<uint64_t> levels, mine(1 << 12), gen(1 << 12);
-  for (int r = 0; r < n; ++r) {
-    int32_t k = 0, kg = 0;
-    if (tlcg_level_sizes(ctxs[(size_t)r], mine.data(), (int32_t)mine.size(), &k) != 0)
-      return fail(r, "tlcg_level_sizes", -1);
-    if (tlcg_level_generated(ctxs[(size_t)r], gen.data(), (int32_t)gen.size(), &kg) != 0)
-      return fail(r, "tlcg_level_generated", -1);
-    k = std::min<int32_t>(k, (int32_t)mine.size());
-    kg = std::min<int32_t>(kg, (int32_t)gen.size());
-    const size_t kk = std::min<size_t>((size_t)k, cut);
-    if (kk > levels.size()) levels.resize(kk, 0);
-    for (size_t i = 0; i < kk; ++i) levels[i] += mine[i];
-    for (size_t i = 0; i < std::min<size_t>((size_t)kg, cut); ++i) out.generated += gen[i];
-  }
-  while (!levels.empty() && !levels.back()) levels.pop_back();
-  for (uint64_t x : levels) out.distinct += x;
-  out.frontier = first < 0 || levels.empty() ? 0 : levels.back();
-  out.status = first < 0 ? TLCG_DONE : sts[(size_t)first].status;
-  out.invariant = first < 0 ? -1 : sts[(size_t)first].invariant;
-  out.action = first < 0 ? -1 : sts[(size_t)first].action;
-  out.event_gidx = first < 0 ? ~0ull : sts[(size_t)first].event_gidx;
-  out.depth = first < 0 ? (int32_t)levels.size() : sts[(size_t)first].depth;
-  const double d = (double)out.distinct, g = (double)out.generated;
-  out.fp_collision_optimistic = d * (g - d) / 18446744073709551616.0;
+  tlcg::LocalBoard* board = rccl ? nullptr : tlcg::local_board_new(ctxs.data(), n);
+  std::vector<tlcg_stats> sts((size_t)n);
+  std::vector<std::vector<uint64_t>> lvs((size_t)n);
+  std::vector<std::string> errs((size_t)n);
+  std::vector<int> rc((size_t)n, 0);
+  std::vector<std::thread> th;
+  for (int r = 0; r < n; ++r)
+    th.emplace_back([&, r] {
+      tlcg::Transport* t = rccl ? tlcg::comm_transport(ctxs[(size_t)r]) : tlcg::local_transport(board, r);
+      rc[(size_t)r] = tlcg::run_ranks(ctxs[(size_t)r], *t, &sts[(size_t)r], &lvs[(size_t)r], &errs[(size_t)r]);
+    });
+  for (auto& t : th) t.join();
+  tlcg::local_board_free(board);
+  for (int r = 0; r < n; ++r)
+    if (rc[(size_t)r]) {
+      put_err(err, err_cap, "rank " + std::to_string(r) + ": " + errs[(size_t)r]);
+      destroy_all();
+      return rc[(size_t)r];
+    }
+  // every rank holds the combined result
+  *st = sts[0];
+  st->transport = rccl ? 2 : 1;
+  const auto& lv = lvs[0];
   if (levels_out)
-    for (size_t i = 0; i < levels.size() && (int32_t)i < cap; ++i) levels_out[i] = levels[i];
-  if (n_levels) *n_levels = (int32_t)levels.size();
-  for (auto* c : ctxs) tlcg_destroy(c);
-  *st = out;
+    for (size_t i = 0; i < lv.size() && (int32_t)i < cap; ++i) levels_out[i] = lv[i];
+  if (n_levels) *n_levels = (int32_t)lv.size();
+  destroy_all();
   return 0;
 }

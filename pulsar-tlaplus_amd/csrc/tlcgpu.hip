@@ -22,6 +22,7 @@
 #include <sys/mman.h>
 
 #include "component.h"
+#include "exchange.h"
 #include "host_model.h"
 #include "jit.h"
 #include "kernels.h"
@@ -736,7 +737,18 @@ struct tlcg_ctx {
   u64 owner_mask = ~0ull;
   std::string err;
   bool inited = false;
+  void* comm = nullptr;  // RCCL state (exchange.cpp), tlcg_comm_init
 };
+
+namespace tlcg {
+int ctx_device(const tlcg_ctx* c) { return c->opts.device; }
+void ctx_rank_world(const tlcg_ctx* c, int* rank, int* world) {
+  *rank = c->opts.rank;
+  *world = c->opts.world;
+}
+void*& ctx_comm(tlcg_ctx* c) { return c->comm; }
+void ctx_set_error(tlcg_ctx* c, const std::string& e) { c->err = e; }
+}  // namespace tlcg
 
 namespace {
 
@@ -2063,6 +2075,8 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
 void tlcg_destroy(tlcg_ctx* c) {
   if (!c) return;
   const DeviceGuard dg(c);
+  tlcg::comm_free(c->comm);
+  c->comm = nullptr;
   if (c->stream) hipStreamSynchronize(c->stream);
   hipFree(c->d_slots);
   hipFree(c->d_dkey_slot);

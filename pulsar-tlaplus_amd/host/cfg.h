@@ -42,6 +42,7 @@ struct Def {
 
 struct Module {
   std::string name;
+  bool builtin = false;  // built from known_defs.inc (no .tla text): fingerprints + extents only
   std::vector<Def> defs;
   std::map<std::string, size_t> by_name;
   int assume_l0 = 0, assume_c0 = 0, assume_l1 = 0, assume_c1 = 0;
@@ -52,6 +53,11 @@ struct Module {
 };
 
 bool parse_module(const std::string& text, Module* out, std::string* err);
+
+// The module this build implements, from its compiled-in table (definition
+// names, body fingerprints and source extents of compaction.tla -- numbers,
+// not text): what tlc-hip checks when no .tla is given.
+Module builtin_module();
 
 // Checks that the module is the compaction spec this build implements
 // (operator bodies compared after normalization); lists differing ones.

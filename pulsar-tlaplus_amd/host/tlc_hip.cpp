@@ -72,7 +72,8 @@ void usage() {
   std::fprintf(stderr,
                "usage: tlc-hip [-config FILE.cfg] [-deadlock] [-workers N] [-gpu D | -gpus N] [-fpbits B]\n"
                "               [-checkpoint MINUTES] [-metadir DIR] [-recover DIR]\n"
-               "               [-tlc-order] [-no-trace] [-json] [-dump-defs] SPEC.tla\n");
+               "               [-tlc-order] [-no-trace] [-json] [-dump-defs] [SPEC.tla]\n"
+               "  without SPEC.tla: the built-in compaction module, with -config FILE.cfg\n");
 }
 
 struct Opts {
@@ -146,22 +147,31 @@ int main(int argc, char** argv) {
     else if (!a.empty() && a[0] == '-') { std::fprintf(stderr, "Error: unsupported option %s\n", a.c_str()); usage(); return 255; }
     else o.spec = a;
   }
-  if (o.spec.empty()) { usage(); return 255; }
+  // no SPEC.tla: check the built-in module (the definitions of compaction.tla
+  // as this build implements them), the cfg given by -config
+  const bool builtin = o.spec.empty() && !o.cfg.empty() && !o.dump_defs;
+  if (o.spec.empty() && !builtin) { usage(); return 255; }
   if (o.gpus < 1 || o.gpus > 64) { std::fprintf(stderr, "Error: -gpus needs 1..64\n"); return 255; }
   if (o.gpus > 1 && !o.recover.empty()) { std::fprintf(stderr, "Error: -recover runs on one GPU\n"); return 255; }
   if (o.gpus > 1) o.checkpoint_min = 0;  // checkpoints hold one context's levels
+  if (builtin) o.spec = "compaction.tla";
   if (o.spec.size() < 4 || o.spec.substr(o.spec.size() - 4) != ".tla") o.spec += ".tla";
   if (o.cfg.empty()) o.cfg = o.spec.substr(0, o.spec.size() - 4) + ".cfg";
 
   std::string tla, cfgtext, err;
-  if (!read_file(o.spec, &tla)) { std::printf("Error: cannot read %s\n", o.spec.c_str()); return 255; }
   Module mod;
-  if (!parse_module(tla, &mod, &err)) { std::printf("Error: %s\n", err.c_str()); return 150; }
+  if (builtin) {
+    mod = builtin_module();
+  } else {
+    if (!read_file(o.spec, &tla)) { std::printf("Error: cannot read %s\n", o.spec.c_str()); return 255; }
+    if (!parse_module(tla, &mod, &err)) { std::printf("Error: %s\n", err.c_str()); return 150; }
+  }
   if (o.dump_defs) {  // maintenance: fingerprints for known_defs.inc
     for (auto& d : mod.defs) {
       uint64_t h = 1469598103934665603ull;
       for (unsigned char c : d.norm) { h ^= c; h *= 1099511628211ull; }
-      std::printf("    {\"%s\", 0x%016llxull},\n", d.name.c_str(), (unsigned long long)h);
+      std::printf("    {\"%s\", 0x%016llxull, %d, %d, %d, %d},\n", d.name.c_str(), (unsigned long long)h, d.line0,
+                  d.col0, d.line1, d.col1);
     }
     return 0;
   }
@@ -173,7 +183,8 @@ int main(int argc, char** argv) {
                 o.gpus, std::max(1, tlcg_device_count()));
   else
     std::printf("Running breadth-first search Model-Checking with 1 GPU (device %d) and seed 0.\n", o.gpu);
-  std::printf("Parsing file %s\n", o.spec.c_str());
+  if (builtin) std::printf("Parsing file %s (built-in: the definitions of compaction.tla this build implements)\n", o.spec.c_str());
+  else std::printf("Parsing file %s\n", o.spec.c_str());
   if (!recognize_compaction(mod, &err)) { std::printf("Error: %s\n", err.c_str()); return 150; }
   if (!read_file(o.cfg, &cfgtext)) { std::printf("Error: cannot read configuration file %s\n", o.cfg.c_str()); return 150; }
   Config cfg;

@@ -155,6 +155,38 @@ def _reduce_result(engine, stats, group, dev: torch.device) -> DistResult:
                       invariant=inv_all if inv_all >= 0 else None, first_error_rank=first)
 
 
+def init_native(engine: "GpuEngine", group=None) -> None:
+    """An RCCL communicator inside libtlcgpu for this rank (tlcg_comm_init):
+    rank 0 makes the id, the group broadcasts it."""
+    lib = engine.lib
+    buf = C.create_string_buffer(128)
+    if dist.get_rank(group) == 0:
+        n = lib.tlcg_comm_unique_id(buf, 128)
+        if n != 128:
+            raise RuntimeError(f"tlcg_comm_unique_id: {n} (RCCL available: {lib.tlcg_comm_available()})")
+    obj = [buf.raw]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    buf = C.create_string_buffer(obj[0], 128)
+    engine.ck._chk(lib.tlcg_comm_init(engine.ctx, buf, 128), "tlcg_comm_init")
+
+
+def run_native(engine: "GpuEngine") -> DistResult:
+    """The whole check inside libtlcgpu (tlcg_run_comm): the level loop and its
+    exchange run in C++ over RCCL -- all-gather of the per-destination counts,
+    grouped send/recv of the records on the context's stream, all-reduce for
+    termination and the combined result -- with no Python in the level loop.
+    init_native() first."""
+    lib = engine.lib
+    st = tlcgpu.tlcg_stats()
+    lv = (C.c_uint64 * 65536)()
+    n = C.c_int32()
+    engine.ck._chk(lib.tlcg_run_comm(engine.ctx, C.byref(st), lv, 65536, C.byref(n)), "tlcg_run_comm")
+    levels = [lv[i] for i in range(n.value)]
+    return DistResult(status=tlcgpu.STATUS[st.status], generated=st.generated, distinct=st.distinct, depth=st.depth,
+                      levels=levels, kernel_ms=st.kernel_ms, expand_ms=st.expand_ms, closed=engine.closed,
+                      invariant=st.invariant if st.invariant >= 0 else None)
+
+
 def _transport_device(group, dev: torch.device) -> torch.device:
     """Where exchanged records live: on the GPU for RCCL (nccl backend, xGMI),
     in host memory for gloo (rehearsals of the same level loop)."""

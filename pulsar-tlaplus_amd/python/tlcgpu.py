@@ -53,7 +53,8 @@ class tlcg_stats(C.Structure):
                 ("depth", C.c_int32), ("status", C.c_int32), ("invariant", C.c_int32), ("action", C.c_int32),
                 ("event_gidx", C.c_uint64), ("fp_collision_optimistic", C.c_double), ("kernel_ms", C.c_double),
                 ("expand_ms", C.c_double), ("levels_redone", C.c_uint64), ("engine", C.c_uint64),
-                ("jit_used", C.c_uint64), ("host_states", C.c_uint64), ("fpset_host_states", C.c_uint64)]
+                ("jit_used", C.c_uint64), ("host_states", C.c_uint64), ("fpset_host_states", C.c_uint64),
+                ("transport", C.c_uint64)]
 
 
 _lib = None
@@ -120,6 +121,10 @@ def load_library(path: str = LIB_PATH):
         "tlcg_exchange_local": (C.c_int, [C.POINTER(P), I32, C.POINTER(U64)]),
         "tlcg_partition_closed": (C.c_int, [P]),
         "tlcg_run_node": (C.c_int, [M, O, I32, S, C.POINTER(U64), I32, C.POINTER(I32), C.c_char_p, I32]),
+        "tlcg_comm_available": (C.c_int, []),
+        "tlcg_comm_unique_id": (C.c_int, [P, I32]),
+        "tlcg_comm_init": (C.c_int, [P, P, I32]),
+        "tlcg_run_comm": (C.c_int, [P, S, C.POINTER(U64), I32, C.POINTER(I32)]),
         "tlcg_jit_selftest": (C.c_int, [M, C.c_char_p, I32, C.c_char_p, I32][:1] + [C.c_char_p, C.c_char_p, I32]),
     }
     for name, (res, args) in sig.items():
@@ -277,6 +282,7 @@ class Result:
     host_states: int = 0
     fpset_host_states: int = 0
     trace: List[Tuple[str, int]] = field(default_factory=list)
+    transport: str = ""  # multi-rank runs: "local" (threads, device copies) or "rccl"
 
 
 class Checker:
@@ -447,7 +453,8 @@ def run_node(model: Model, ranks: int, device: int = 0, log2_fpset_slots: int = 
                left_on_queue=0 if status == "ok" else st.frontier, levels=[lv[i] for i in range(n.value)],
                collision_optimistic=st.fp_collision_optimistic, kernel_ms=st.kernel_ms, expand_ms=st.expand_ms,
                levels_redone=st.levels_redone, engine={v: k for k, v in ENGINES.items()}.get(st.engine, "?"),
-               host_states=st.host_states, fpset_host_states=st.fpset_host_states)
+               host_states=st.host_states, fpset_host_states=st.fpset_host_states,
+               transport={1: "local", 2: "rccl"}.get(st.transport, ""))
     if st.invariant >= 0:
         r.invariant = model.invariants[st.invariant]
     if st.action >= 0:

@@ -80,3 +80,38 @@ def test_checkpoint_refusals(tmp_path):
     with pytest.raises(RuntimeError, match="cannot read"):
         other.recover(str(tmp_path / "missing.ckpt"))
     other.close()
+
+
+@pytest.mark.parametrize("damage", ["truncate", "levels", "distinct"])
+def test_corrupt_checkpoint_is_refused(tmp_path, damage):
+    """a truncated or corrupt checkpoint is refused with -3 before
+    anything is sized from its header (no allocation from a bad count)."""
+    import ctypes as C
+    import struct
+    path = tmp_path / "ck"
+    m = model_of(GOLDEN["S"]["constants"])
+    a = tlcgpu.Checker(m, engine="global")
+    try:
+        a.init()
+        for _ in range(5):
+            a.step_level()
+        a.checkpoint(str(path))
+    finally:
+        a.close()
+    raw = bytearray(path.read_bytes())
+    hdr = struct.calcsize("8s8i4Q2d")
+    if damage == "truncate":
+        raw = raw[: len(raw) - 24]
+    elif damage == "levels":  # n_levels = 2^60
+        struct.pack_into("Q", raw, 8 + 32, 1 << 60)
+    else:  # distinct (and the last level base) beyond the file
+        struct.pack_into("Q", raw, 8 + 32 + 24, 1 << 40)
+    assert hdr == 8 + 32 + 32 + 16
+    path.write_bytes(bytes(raw))
+    b = tlcgpu.Checker(m, engine="global")
+    try:
+        st = tlcgpu.tlcg_stats()
+        assert b.lib.tlcg_recover(b.ctx, str(path).encode(), C.byref(st)) == -3
+        assert b"corrupt" in b.lib.tlcg_last_error(b.ctx)
+    finally:
+        b.close()

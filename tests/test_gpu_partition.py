@@ -110,3 +110,87 @@ def test_run_node_matches_checker_engines():
     for engine in ("auto", "global", "component"):
         r = tlcgpu.run_node(m, 4, engine=engine)
         assert (r.generated, r.distinct, r.levels) == (want["generated"], want["distinct"], want["levels"])
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+@pytest.mark.parametrize("case,partition", [("V_leak", 0), ("V_dup", 0), ("V_leak_producer", 0), ("V_leak", 2)])
+def test_run_node_error_counts_at_level_end(case, partition, ranks):
+    """every rank's counts cut at the end of the first error's level: the
+    counts one context reports (the oracles' eol_* numbers)"""
+    want = GOLDEN[case]["result"]
+    r = tlcgpu.run_node(model_of(GOLDEN[case]["constants"]), ranks, partition=partition)
+    assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+    assert r.levels[:-1] == want["levels"][:-1] and sum(r.levels) == r.distinct
+    assert r.transport == "local"  # ranks share the one GPU
+
+
+# SURVEY App.A.2: distinct states per BFS level of one initial message sequence
+PER_M_LEVELS = [1, 2, 2, 3, 3, 3, 4, 3, 3, 4, 4, 3, 4, 4, 4, 5, 5, 1, 2, 2]
+
+
+def test_g9_hash_partitioned_8_ranks():
+    """BASELINE config 4 on one GPU: G9 (~1e9 states) with the FPSet
+    partitioned on the whole state (owner = mix64(state), partition 2) over 8
+    ranks, so every BFS level runs expand -> all-to-all of records -> absorb
+    (tlcg_run_node, the level loop of tlcg_run_comm with the local transport).
+    Exact counts, depth and per-level sizes."""
+    m = tlcgpu.Model(key_space=range(1, 16), value_space=range(1, 16))
+    per = 1_040_187_392 // 8 + 1
+    r = tlcgpu.run_node(m, 8, partition=2, engine="global", log2_fpset_slots=(2 * per - 1).bit_length(),
+                        state_capacity=int(per * 1.1) + (1 << 20))
+    assert (r.status, r.generated, r.distinct, r.depth) == ("ok", 1_392_508_928, 1_040_187_392, 20)
+    assert r.levels == [16 ** 6 * x for x in PER_M_LEVELS]
+    assert r.transport == "local"
+
+
+@pytest.mark.parametrize("case,partition", [("S", 0), ("P_published", 0), ("V_leak", 0), ("V_leak_producer", 0)])
+def test_run_node_rccl_transport(case, partition, monkeypatch):
+    """the RCCL transport (ncclCommInitAll, all-reduces of the combine) with
+    one rank on the one GPU of the box; the driver's 8-GPU node runs it with
+    records moving over xGMI"""
+    monkeypatch.setenv("TLCG_NODE_TRANSPORT", "rccl")
+    want = GOLDEN[case]["result"]
+    r = tlcgpu.run_node(model_of(GOLDEN[case]["constants"]), 1, partition=partition)
+    assert r.transport == "rccl"
+    assert r.status == want["result"]
+    if want["result"] == "ok":
+        assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                                 want["levels"])
+    else:
+        assert (r.generated, r.distinct, r.depth) == (want["eol_generated"], want["eol_distinct"], want["depth"])
+
+
+def test_native_comm_world1():
+    """tlcg_comm_unique_id -> tlcg_comm_init -> tlcg_run_comm (what
+    dist.run_native drives per process), twice on one communicator"""
+    import ctypes as C
+    m = model_of(GOLDEN["P_published"]["constants"])
+    want = GOLDEN["P_published"]["result"]
+    ck = tlcgpu.Checker(m)
+    try:
+        lib = ck.lib
+        assert lib.tlcg_comm_available() == 1
+        buf = C.create_string_buffer(128)
+        assert lib.tlcg_comm_unique_id(buf, 128) == 128
+        assert lib.tlcg_comm_init(ck.ctx, buf, 128) == 0, lib.tlcg_last_error(ck.ctx)
+        for _ in range(2):
+            st = tlcgpu.tlcg_stats()
+            lv = (C.c_uint64 * 4096)()
+            n = C.c_int32()
+            assert lib.tlcg_run_comm(ck.ctx, C.byref(st), lv, 4096, C.byref(n)) == 0, lib.tlcg_last_error(ck.ctx)
+            assert (st.generated, st.distinct, st.depth, st.transport) == (want["generated"], want["distinct"],
+                                                                           want["depth"], 2)
+            assert [lv[i] for i in range(n.value)] == want["levels"]
+    finally:
+        ck.close()
+
+
+def test_run_comm_without_communicator_is_refused():
+    import ctypes as C
+    ck = tlcgpu.Checker(tlcgpu.Model())
+    try:
+        st = tlcgpu.tlcg_stats()
+        assert ck.lib.tlcg_run_comm(ck.ctx, C.byref(st), None, 0, None) < 0
+        assert b"no communicator" in ck.lib.tlcg_last_error(ck.ctx)
+    finally:
+        ck.close()
