@@ -492,9 +492,10 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
   }
   if (trace)
     std::fprintf(stderr,
-                 "rank %d: %d levels, wall s: flags %.3f expand %.3f counts %.3f inbox %.3f records %.3f absorb %.3f "
-                 "end %.3f\n",
-                 me, nlev, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6]);
+                 "rank %d: %d levels (%llu redone), wall s: flags %.3f expand %.3f counts %.3f inbox %.3f records %.3f "
+                 "absorb %.3f end %.3f; device ms: kernels %.1f expand %.1f\n",
+                 me, nlev, (unsigned long long)s.levels_redone, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6],
+                 s.kernel_ms, s.expand_ms);
   // ---- combine, like one context's level loop would report ----
   std::vector<uint64_t> mine(1u << 16), gen(1u << 16);
   int32_t k = 0, kg = 0;

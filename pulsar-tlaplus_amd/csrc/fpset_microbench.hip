@@ -32,18 +32,36 @@ __device__ __forceinline__ u64 mix(u64 x) {
   return x;
 }
 
+// the XCD (0..7) this wave runs on
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7u;
+}
+
+// KIND 6..8: the table split into 8 partitions, each block touching only the
+// partition of the XCD it runs on (slots stay in that XCD's L2):
+//   6 cas_wg_xcd     workgroup-scope CAS (performed in the XCD's L2)
+//   7 cas_agent_xcd  device-scope CAS (performed at the memory side)
+//   8 load_xcd       plain load
 template <int KIND>
 __global__ __launch_bounds__(256) void k_access(u64* __restrict__ t, int log2, u64 n, u64 seed, u64* sink) {
   const int sh = 64 - log2;
   u64 acc = 0;
+  const u64 part = (u64)xcc_id() << (log2 - 3);
   for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) {
     const u64 h = mix(i ^ seed);
-    const u64 s = h >> sh;
+    const u64 s = KIND >= 6 ? part | (h >> (sh + 3)) : h >> sh;
     if (KIND == 0) acc += t[s];
     else if (KIND == 1) acc += __builtin_nontemporal_load(&t[s]);
     else if (KIND == 2) t[s] = h | 1;
-    else if (KIND == 3) acc += atomicCAS(&t[s], 0ull, h | 1);
-    else if (KIND == 4) acc += atomicCAS(&t[s], 0ull, h | 1);
+    else if (KIND == 3 || KIND == 4 || KIND == 7) acc += atomicCAS(&t[s], 0ull, h | 1);
+    else if (KIND == 6) {
+      u64 e = 0;
+      __hip_atomic_compare_exchange_strong(&t[s], &e, h | 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      acc += e;
+    } else if (KIND == 8) acc += t[s];
     else atomicAdd(&t[s], 1ull);
   }
   if (acc == 0x123456789ull) *sink = acc;
@@ -52,6 +70,7 @@ __global__ __launch_bounds__(256) void k_access(u64* __restrict__ t, int log2, u
 int main(int argc, char** argv) {
   int log2 = argc > 1 ? std::atoi(argv[1]) : 31;
   u64 n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1ull << 30);
+  const int first_kind = argc > 3 ? std::atoi(argv[3]) : 0;
   u64* t;
   u64* sink;
   CHK(hipMalloc(&t, 8ull << log2));
@@ -59,9 +78,10 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
-  const char* names[] = {"load", "load_nt", "store", "cas_new", "cas_old", "add"};
+  const char* names[] = {"load", "load_nt", "store", "cas_new", "cas_old", "add", "cas_wg_xcd", "cas_agent_xcd",
+                         "load_xcd"};
   for (int grid : {4096, 16384}) {
-    for (int kind = 0; kind < 6; ++kind) {
+    for (int kind = first_kind; kind < 9; ++kind) {
       // cas_new wants empty slots at the probed positions, the others do not care
       CHK(hipMemset(t, 0, 8ull << log2));
       if (kind == 4) {  // pre-fill the slots cas_old will hit
@@ -75,7 +95,10 @@ int main(int argc, char** argv) {
         case 2: k_access<2><<<grid, 256>>>(t, log2, n, 7, sink); break;
         case 3: k_access<3><<<grid, 256>>>(t, log2, n, 7, sink); break;
         case 4: k_access<4><<<grid, 256>>>(t, log2, n, 7, sink); break;
-        default: k_access<5><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        case 5: k_access<5><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        case 6: k_access<6><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        case 7: k_access<7><<<grid, 256>>>(t, log2, n, 7, sink); break;
+        default: k_access<8><<<grid, 256>>>(t, log2, n, 7, sink); break;
       }
       CHK(hipEventRecord(b));
       CHK(hipEventSynchronize(b));

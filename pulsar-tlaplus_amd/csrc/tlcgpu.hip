@@ -53,10 +53,14 @@ struct ExpandArgs {
 };
 
 // owner rank of a state: wide states are only partitioned by `messages`,
-// which then lies in the low word (tlcg_create checks)
+// which then lies in the low word (tlcg_create checks).  The LOW 32 bits of
+// the mix pick the owner: FPSet slots come from its high bits, and with the
+// whole state as the partition key (partition 2) an owner taken from the high
+// bits would leave every rank's states in 1/world of its table.
+TLCG_HD int owner_hash(u64 key, int world) { return (int)(((mix64(key) & 0xFFFFFFFFull) * (u64)world) >> 32); }
 template <typename W>
 __device__ __forceinline__ int owner_of(W s, u64 owner_mask, int world) {
-  return (int)(((mix64((u64)s & owner_mask) >> 32) * (u64)world) >> 32);
+  return owner_hash((u64)s & owner_mask, world);
 }
 
 // overflow flag of a failed FPSet insert
@@ -2714,7 +2718,7 @@ int tlcg_device_count(void) {
 
 int tlcg_owner(tlcg_ctx* c, uint64_t state) {
   if (!c) return -1;  // wide states: pass the low word (the partition key lies there)
-  return (int)(((mix64(state & c->owner_mask) >> 32) * (u64)c->opts.world) >> 32);
+  return owner_hash(state & c->owner_mask, c->opts.world);
 }
 
 // ---- partitioned levels (world > 1) ----
@@ -2736,8 +2740,13 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
   c->pending = 0;
   if (!ensure_store(c, d + std::min(worst, std::max(est, (u64)1 << 20)))) return -10;
   if ((c->opts.log2_fpset_slots <= 0 || c->opts.fpset_spill) && !ensure_fpset(c, d + est)) return -10;
-  // outbox: an even split of the expected successors, with slack; grows on overflow
+  // outbox: an even split of the expected successors, with slack, at least a
+  // share of the planned store (opts.state_capacity); it only grows, doubling
+  // (a hipFree / hipMalloc between levels stalls every queue of the device,
+  // the other ranks' kernels included)
   u64 per_dst = F ? 2 * est / (u64)c->opts.world + 1024 : 1024;
+  per_dst = std::max<u64>(per_dst, c->opts.state_capacity / (2 * (u64)c->opts.world));
+  if (per_dst > c->outbox_cap) per_dst = std::max<u64>(per_dst, 2 * c->outbox_cap);
   for (;;) {
     if (per_dst > c->outbox_cap) {
       hipFree(c->d_outbox);
@@ -2761,6 +2770,10 @@ int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
     }
     const unsigned ovf = c->h_ctr->overflow;
     if (!ovf) break;
+    if (std::getenv("TLCG_RANK_TRACE"))
+      std::fprintf(stderr, "rank %d level %d: expand overflow %u (outbox cap %llu, store room %llu, log2 %d)\n",
+                   c->opts.rank, depth, ovf, (unsigned long long)c->outbox_cap, (unsigned long long)dev_room(c, d),
+                   c->log2);
     // grow what overflowed and redo the expansion from the committed levels
     ++c->levels_redone;
     if (ovf & OVF_OUTBOX) {
@@ -2792,8 +2805,9 @@ int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records) {
   if (n_records > c->inbox_cap) {
     hipFree(c->d_inbox);
     c->d_inbox = nullptr;
+    // doubling, from a share of the planned store (see the outbox in tlcg_expand)
+    u64 ncap = std::max<u64>({n_records + n_records / 4, 4096, 2 * c->inbox_cap, c->opts.state_capacity / 8});
     c->inbox_cap = 0;
-    u64 ncap = std::max<u64>(n_records + n_records / 4, 4096);
     if (!alloc_bytes(c, (void**)&c->d_inbox, ncap * 16, "inbox")) return -10;
     c->inbox_cap = ncap;
   }
@@ -2828,6 +2842,9 @@ int tlcg_absorb(tlcg_ctx* c, uint64_t n_records, tlcg_stats* st) {
     c->kernel_ms += ms;
     const unsigned ovf = c->h_ctr->overflow;
     if (!ovf) break;
+    if (std::getenv("TLCG_RANK_TRACE"))
+      std::fprintf(stderr, "rank %d: absorb overflow %u (records %llu, store room %llu, log2 %d)\n", c->opts.rank,
+                   ovf, (unsigned long long)n_records, (unsigned long long)dev_room(c, d), c->log2);
     // grow and redo: forget this absorb's appends and inserts
     ++c->levels_redone;
     if ((ovf & OVF_STORE) && !ensure_store(c, d + local_new + n_records)) return -10;

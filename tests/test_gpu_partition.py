@@ -141,6 +141,9 @@ def test_g9_hash_partitioned_8_ranks():
     assert (r.status, r.generated, r.distinct, r.depth) == ("ok", 1_392_508_928, 1_040_187_392, 20)
     assert r.levels == [16 ** 6 * x for x in PER_M_LEVELS]
     assert r.transport == "local"
+    # owner and FPSet slot come from independent hash bits: each rank's table at
+    # load 1/2 never overflows, so no level is redone
+    assert r.levels_redone == 0
 
 
 @pytest.mark.parametrize("case,partition", [("S", 0), ("P_published", 0), ("V_leak", 0), ("V_leak_producer", 0)])
