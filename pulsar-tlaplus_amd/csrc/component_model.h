@@ -166,6 +166,50 @@ TLCG_HD int compactor_step_k(const Layout& L, const CompMsgs& c, u64 msgs, lkey 
   return 0;
 }
 
+// The same disjunct without branches on compactorState: every phase's
+// successor is formed and the one of `ph` selected, so the lanes of a wave
+// never diverge here (same results as compactor_step_k; the selfcheck and the
+// golden tests run whichever the kernel uses).
+TLCG_HD int compactor_step_k_sel(const Layout& L, const CompMsgs& c, u64 msgs, lkey k, int ph, lkey* t, int* act) {
+  const int p1r = k_p1r(L, k);
+  const int m = k_max_ledger(L, k);
+  const lkey to_ph = ~(lmask(3) << (L.ph_sh - L.led_sh));
+  const lkey base = k & to_ph;
+  auto with_ph = [&](lkey x, int p) { return (x & to_ph) | ((lkey)p << (L.ph_sh - L.led_sh)); };
+  // PhaseOne (:93-100)
+  const lkey t_one = with_ph(lset(L, base, L.p1r_sh, L.p1r_w, (lkey)c.len), PH_WRITE);
+  const bool en_one = p1r == 0 && c.len > 0;
+  // PhaseTwoWrite (:121-132); p1r <= N: the precomputed CompactMessages
+  const int nid = m + 1;
+  const int r1 = p1r > 0 ? p1r - 1 : 0;
+  u64 mask = (c.cm >> (r1 * L.N)) & nmask(L.N);
+  if (p1r > L.N) mask = compact_mask(L, msgs | ((u64)k << L.led_sh), p1r);
+  const int nid_c = nid <= L.C ? nid : L.C;  // (a disabled Write forms a dummy ledger)
+  const lkey t_write = with_ph(lset(L, base, led_base(L, nid_c), L.led_w, (lkey)(1ull | (mask << 1))), PH_UCTX);
+  const bool en_write = p1r != 0 && nid <= L.C;
+  // UpdateContext (:135-139), UpdateHorizon (:141-145)
+  const lkey t_uctx = with_ph(lset(L, base, L.ctx_sh, L.ctx_w, (lkey)m), PH_UHOR);
+  const lkey t_uhor = with_ph(lset(L, base, L.hz_sh, L.hz_w, (lkey)p1r), PH_PERSIST);
+  // PersistCusror (:147-151)
+  const lkey cur = 1u | ((lkey)k_hz(L, k) << 1) | ((lkey)k_ctx(L, k) << (1 + L.curh_w));
+  const lkey t_pers = with_ph(lset(L, base, L.cur_sh, 1 + L.curh_w + L.curc_w, cur), PH_DELETE);
+  // DeleteLedger (:153-165): ledger m - 1 cleared unless m = 1
+  const lkey d0 = with_ph(lset(L, base, L.p1r_sh, L.p1r_w, 0), PH_ONE);
+  const int old = m - 1 >= 1 ? m - 1 : 1;
+  const lkey t_del = m != 1 ? lset(L, d0, led_base(L, old), L.led_w, 0) : d0;
+  lkey r = t_one;
+  int a = ACT_PHASEONE, res = en_one ? 1 : 0;
+  if (ph == PH_WRITE) { r = t_write; a = ACT_WRITE; res = en_write ? 1 : 0; }
+  if (ph == PH_UCTX) { r = t_uctx; a = ACT_UCTX; res = 1; }
+  if (ph == PH_UHOR) { r = t_uhor; a = ACT_UHOR; res = p1r == 0 ? 2 : 1; }
+  if (ph == PH_PERSIST) { r = t_pers; a = ACT_PERSIST; res = 1; }
+  if (ph == PH_DELETE) { r = t_del; a = ACT_DELETE; res = m != 1 && m - 1 < 1 ? 2 : 1; }
+  if (ph > PH_DELETE) res = 0;
+  *t = r;
+  if (res) *act = a;
+  return res;
+}
+
 // BrokerCrash, compaction.tla:169-182.  Returns 1 if enabled.
 TLCG_HD int crash_step_k(const Layout& L, lkey k, lkey* t) {
   const int cr = k_crash(L, k);

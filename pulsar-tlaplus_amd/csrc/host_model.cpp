@@ -421,6 +421,10 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
       const int r1 = compactor_step_ph(L, s, st_phase(L, s), &t1, &a1);
       const int r2 = compactor_step_k(L, cm, msgs, k, k_phase(L, k), &t2, &a2);
       const int x1 = crash_step(L, s, &t2w), x2 = crash_step_k(L, k, &c2);
+      lkey t3 = 0;
+      int a3 = -1;
+      const int r3 = compactor_step_k_sel(L, cm, msgs, k, k_phase(L, k), &t3, &a3);  // the branch-free form
+      if (r3 != r1 || a3 != a1 || (r1 == 1 && t3 != t2)) return -(1 + checked);
       if (r1 != r2 || a1 != a2 || (r1 == 1 && t1 != (msgs | ((u64)t2 << mb))) || x1 != x2 ||
           (x1 && t2w != (msgs | ((u64)c2 << mb))) || check_invariants(L, s) != check_invariants_k(L, cm, k) ||
           selfloop_count(L, s) != selfloop_count_k(L, cm, k))
