@@ -37,6 +37,7 @@ struct CompMsgs {
   u64 need;           // horizon witnesses of position i = 1..N: N bits at (i - 1) * N (a position p >= i with key(p) = key(i))
   uint32_t skip;      // positions whose messagesBeforeHorizon entry is Nil (null key, not retained)
   uint32_t null_pos;  // positions 1..Len holding NullKey
+  u64 hwit;           // N <= 4: for each ledger position mask m, the positions it witnesses: N bits at m * N
   int len;            // Len(messages)
   int msgs_ok;        // TypeSafe's messages conjunct (and Len(messages) <= N)
 };
@@ -67,6 +68,13 @@ TLCG_HD CompMsgs comp_msgs_init(const Layout& L, u64 s) {
       c.need |= w << ((i - 1) * L.N);
     }
   }
+  // the witness table: CompactionHorizonCorrectness on a ledger mask m is one
+  // lookup (N x 2^N bits <= 64)
+  c.hwit = 0;
+  if (L.N <= 4)
+    for (u64 m = 0; m < (1ull << L.N); ++m)
+      for (int i = 0; i < L.N; ++i)
+        if (m & ((c.need >> (i * L.N)) & nmask(L.N))) c.hwit |= 1ull << (m * L.N + i);
   return c;
 }
 
@@ -263,7 +271,14 @@ TLCG_HD int inv_horizon_k(const Layout& L, const CompMsgs& c, lkey k) {
     if (ctx < 1 || ctx > L.C || !k_led_present(L, k, ctx)) return EV_ERROR;
     const u64 m = k_led_mask(L, k, ctx);
     uint32_t fail = 0;  // live positions without a witness in the ledger
-    for (int i = 0; i < L.N; ++i) fail |= (uint32_t)((m & ((c.need >> (i * L.N)) & nmask(L.N))) == 0) << i;
+#ifndef TLCG_HWIT_OFF  // (A/B hook: the loop instead of the table)
+    if (L.N <= 4) {
+      fail = ~(uint32_t)(c.hwit >> (m * L.N)) & (uint32_t)nmask(L.N);
+    } else
+#endif
+    {
+      for (int i = 0; i < L.N; ++i) fail |= (uint32_t)((m & ((c.need >> (i * L.N)) & nmask(L.N))) == 0) << i;
+    }
     if (fail & live) return EV_FALSE;
   }
   return EV_TRUE;

@@ -248,8 +248,10 @@ int main(int argc, char** argv) {
                 (unsigned long long)(st.distinct - st.frontier), (unsigned long long)st.frontier);
   } else if (ctx) {
     if (tlcg_init(ctx, &st) != 0) { std::printf("Error: %s\n", tlcg_last_error(ctx)); tlcg_destroy(ctx); return 255; }
-    std::printf("Finished computing initial states: %llu distinct state%s generated at %s.\n",
-                (unsigned long long)st.distinct, st.distinct == 1 ? "" : "s", now_str().c_str());
+    // (the initial states: the component engine has finished the whole search by now)
+    const unsigned long long n0 = (unsigned long long)tlcg_init_count(&model);
+    std::printf("Finished computing initial states: %llu distinct state%s generated at %s.\n", n0, n0 == 1 ? "" : "s",
+                now_str().c_str());
   }
   auto last_progress = std::chrono::steady_clock::now();
   auto last_checkpoint = last_progress;

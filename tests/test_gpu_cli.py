@@ -131,5 +131,7 @@ def test_cli_shipped_string_keys_assume(tmp_path):
     TLC stops on the ASSUME (compaction.tla:25-35) before any state"""
     rc, lines = run(tmp_path, numeric_cfg(KeySpace='{"key1", "key2"}'))
     assert rc == 75
-    assert "Evaluating assumption line 25, col 8 to line 35, col 35 of module compaction failed." in lines
-    assert "Computing initial states..." not in lines
+    text = "\n".join(lines)
+    assert "Evaluating assumption line 25, col 8 to line 35, col 35 of module compaction failed." in text
+    assert 'Attempted to check if the value:\n"key1"\nis an element of Nat.' in text
+    assert "Computing initial states..." not in text
