@@ -19,6 +19,7 @@
 #include <vector>
 #include <chrono>
 #include <thread>
+#include <type_traits>
 #include <sys/mman.h>
 
 #include "component.h"
@@ -423,6 +424,137 @@ __global__ __launch_bounds__(BLOCK) void k_expand_fast(ExpandArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
+  }
+  gen = wave_sum_u64(gen);
+  if (__lane_id() == 0 && gen) atomicAdd(&a.ctr->generated, (unsigned long long)gen);
+  if (ev != NO_EVENT) atomicMin(&a.ctr->event, ev);
+}
+
+// ---- the fast path of a Producer level (discovery order not kept, local
+// partition, one-word states): a thread takes two parents; their successors
+// are probed in chunks whose FPSet probes are all in flight together (a load
+// each, then a CAS on the empty slots), so a thread waits on a chunk of
+// scattered round trips at once instead of one per successor, and the
+// block's LDS stage is flushed once per chunk.  Producer's |KeySet| x
+// |ValueSet| successors (compaction.tla:83-87) come in chunks of PB, and a
+// block none of whose parents can produce (Len(messages) = N: most states)
+// skips them; the compactor and BrokerCrash successors of both parents form
+// one last chunk of four.
+template <int PB>
+__global__ __launch_bounds__(BLOCK) void k_expand_prod(ExpandArgs a) {
+  constexpr int CW = PB > 4 ? PB : 4;  // widest chunk
+  constexpr int CAP = BLOCK * CW;
+  __shared__ u64 s_st[CAP];
+  __shared__ u64 s_par[CAP];
+  __shared__ unsigned s_cnt;
+  __shared__ unsigned long long s_base;
+  const Layout& L = a.L;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  u64 gen = 0;
+  unsigned long long ev = NO_EVENT;
+  const u64 ord_last = (1ull << L.ord_bits) - 1;
+  const int sh = 64 - a.log2;
+  const u64 mask = (1ull << a.log2) - 1;
+  const int ord_crash = ordinal_of(L, ACT_CRASH, 0);
+  // probe, insert, check and stage NC candidates, then flush the stage
+  auto chunk = [&](auto ncw, const u64* cand, const bool* has, const u64* dk) {
+    constexpr int NC = decltype(ncw)::value;
+    u64 pos[NC], v[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pos[c] = mix64(cand[c]) >> sh;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) v[c] = has[c] ? __builtin_nontemporal_load(&a.slots[pos[c]]) : 1;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (has[c] && v[c] == 0)
+        v[c] = atomicCAS((unsigned long long*)&a.slots[pos[c]], 0ull, (unsigned long long)(cand[c] | SLOT_TAG));
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      bool isnew = false;
+      if (has[c]) {
+        const u64 key = cand[c] | SLOT_TAG;
+        if (v[c] == 0) {
+          isnew = true;
+        } else if (v[c] != key) {  // the first slot holds another state: probe on
+          u64 slot;
+          const int rr = fpset_put_from(a.slots, mask, key, (pos[c] + 1) & mask, &slot);
+          if (rr < 0) atomicOr(&a.ctr->overflow, (unsigned)OVF_FPSET);
+          isnew = rr == 1;
+        }
+        if (isnew) {
+          const int q = check_invariants(L, cand[c]);
+          if (q >= 0) ev = min(ev, (unsigned long long)make_event(dk[c], (q & 1) ? EVK_INV_ERROR : EVK_VIOLATION, q >> 1));
+        }
+      }
+      stage_append<false, u64>(isnew, cand[c], a.rank_tag | dk[c], 0, s_st, s_par, nullptr, &s_cnt);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&a.ctr->n_new, (unsigned long long)s_cnt) : 0;
+    __syncthreads();
+    const unsigned n = s_cnt;
+    const u64 b = s_base;
+    if (b + n <= a.cap_out) {
+      for (unsigned i = threadIdx.x; i < n; i += BLOCK) {
+        a.states_out[b + i] = s_st[i];
+        a.parents_out[b + i] = s_par[i];
+      }
+    } else if (threadIdx.x == 0 && n) {
+      atomicOr(&a.ctr->overflow, (unsigned)OVF_STORE);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using IPB = std::integral_constant<int, PB>;
+  for (u64 c0 = (u64)blockIdx.x * BLOCK * 2; c0 < a.n_front; c0 += (u64)gridDim.x * BLOCK * 2) {
+    u64 s[2], dk0[2], t[2], t2[2];
+    int len[2], act[2];
+    bool can[2], en1[2], en2[2];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const u64 pi = c0 + (u64)it * BLOCK + threadIdx.x;
+      const bool valid = pi < a.n_front;
+      s[it] = valid ? a.frontier[pi] : 0;
+      dk0[it] = (a.front_gidx0 + pi) << L.ord_bits;
+      len[it] = st_len(L, s[it]);
+      can[it] = valid && len[it] < L.N;  // Producer's guard, :84
+      t[it] = 0;
+      act[it] = 0;
+      const int r = valid ? compactor_step(L, s[it], &t[it], &act[it]) : 0;
+      if (r == 2)
+        ev = min(ev, (unsigned long long)make_event(dk0[it] | (u64)ordinal_of(L, act[it], 0), EVK_ACTION_ERROR, act[it]));
+      en1[it] = r == 1;
+      t2[it] = 0;
+      en2[it] = valid && crash_step(L, s[it], &t2[it]);
+      const int nsucc = (can[it] ? L.nkv : 0) + (int)en1[it] + (int)en2[it] + (valid ? selfloop_count(L, s[it]) : 0);
+      gen += (u64)nsucc;
+      if (valid && nsucc == 0 && L.check_deadlock)
+        ev = min(ev, (unsigned long long)make_event(dk0[it] | ord_last, EVK_DEADLOCK, 0));
+    }
+    if (__syncthreads_or(can[0] || can[1])) {  // block-uniform
+#pragma unroll 1
+      for (int it = 0; it < 2; ++it)
+#pragma unroll 1
+        for (int j0 = 0; j0 < L.nkv; j0 += PB) {
+          u64 cand[PB], dk[PB];
+          bool has[PB];
+#pragma unroll
+          for (int c = 0; c < PB; ++c) {
+            const int j = j0 + c;
+            has[c] = can[it] && j < L.nkv;
+            cand[c] = has[c] ? producer_succ(L, s[it], len[it], j) : 0;
+            dk[c] = dk0[it] | (u64)j;
+          }
+          chunk(IPB(), cand, has, dk);
+        }
+    }
+    const u64 cand[4] = {t[0], t2[0], t[1], t2[1]};
+    const bool has[4] = {en1[0], en2[0], en1[1], en2[1]};
+    const u64 dk[4] = {dk0[0] | (u64)ordinal_of(L, act[0], 0), dk0[0] | (u64)ord_crash,
+                       dk0[1] | (u64)ordinal_of(L, act[1], 0), dk0[1] | (u64)ord_crash};
+    chunk(I4(), cand, has, dk);
   }
   gen = wave_sum_u64(gen);
   if (__lane_id() == 0 && gen) atomicAdd(&a.ctr->generated, (unsigned long long)gen);
@@ -1856,6 +1988,11 @@ bool launch_expand(tlcg_ctx* c, u64 front0, u64 n_front, bool part) {
       else if (it == 2) k_expand_fast<2, 1><<<g, BLOCK, 0, c->stream>>>(a);
       else k_expand_fast<4, 1><<<g, BLOCK, 0, c->stream>>>(a);
     }
+    HIPCHK_I(hipGetLastError());
+    return true;
+  }
+  if (prod && !tlc && !part && c->fast_items > 0 && c->words == 1) {
+    k_expand_prod<8><<<grid_for(n_front, 2 * BLOCK, c->grid_cap), BLOCK, 0, c->stream>>>(a);
     HIPCHK_I(hipGetLastError());
     return true;
   }

@@ -160,12 +160,12 @@ def init_native(engine: "GpuEngine", group=None) -> None:
     rank 0 makes the id, the group broadcasts it."""
     lib = engine.lib
     buf = C.create_string_buffer(128)
-    if dist.get_rank(group) == 0:
-        n = lib.tlcg_comm_unique_id(buf, 128)
-        if n != 128:
-            raise RuntimeError(f"tlcg_comm_unique_id: {n} (RCCL available: {lib.tlcg_comm_available()})")
-    obj = [buf.raw]
-    dist.broadcast_object_list(obj, src=0, group=group)
+    obj = [b""]
+    if dist.get_rank(group) == 0 and lib.tlcg_comm_unique_id(buf, 128) == 128:
+        obj = [buf.raw]
+    dist.broadcast_object_list(obj, src=0, group=group)  # (an empty id: every rank raises below)
+    if len(obj[0]) != 128:
+        raise RuntimeError(f"tlcg_comm_unique_id failed on rank 0 (RCCL available here: {lib.tlcg_comm_available()})")
     buf = C.create_string_buffer(obj[0], 128)
     engine.ck._chk(lib.tlcg_comm_init(engine.ctx, buf, 128), "tlcg_comm_init")
 
