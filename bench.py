@@ -54,6 +54,14 @@ SURVEY_BYTES_PER_DISTINCT = 34.7
 CUS, SIMDS, CLOCK_HZ = 256, 4, 2.4e9
 
 
+def component_kernel_name(jit):
+    """the first-pass component kernel tlcg_stats.jit_used names (bit 0 hipRTC, bit 1 codes)"""
+    if jit & 1:
+        return "tlcg_componentc_64 (hipRTC-specialized, component codes)" if jit & 2 else \
+            "tlcg_component_64 (hipRTC-specialized)"
+    return "k_component<64, codes>" if jit & 2 else "k_component<64>"
+
+
 def load_profile(name):
     """profiles/<newest round>_<name>, or None"""
     import glob
@@ -355,13 +363,14 @@ def main():
         written = COMPONENT_BYTES_PER_STATE * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                  kernel="tlcg_component_64 (hipRTC-specialized)" if r["jit"] else "k_component<64>",
+                  kernel=component_kernel_name(r["jit"]),
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
                   bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
                   kernel_bytes_per_distinct=COMPONENT_BYTES_PER_STATE,
                   kernel_written_gbs=round(written, 1))
         pmc = load_profile(PMC_COMPONENT_PROFILE)
-        if pmc and args.config == "g9" and world == 1 and r["jit"]:
+        # (the counters are of one kernel variant: used only for that variant)
+        if pmc and args.config == "g9" and world == 1 and pmc["kernel"].split()[0] == rf["kernel"].split()[0]:
             c = pmc["counters"]
             kt = r["expand_ms"] * 1e-3
             rf["traffic"] = round(pmc["hbm_bytes_per_step"] / kt / 1e9, 1)

@@ -1,0 +1,256 @@
+// pulsar-tlaplus_amd/csrc/component_code.h -- the spec's per-state functions
+// on *component codes*: a closed component's local keys (component_model.h)
+// re-encoded in about half the bits, so a lane's on-chip queue holds 16-bit
+// entries and a CU holds more lanes.
+//
+// Inside a component `messages` is a constant (component_model.h), and then
+// four fields of the local key can only ever take two values each:
+//   - phaseOneResult.readPosition is Nil or Len(messages): CompactorPhaseOne
+//     is its only writer and writes Len(messages) (compaction.tla:96-97);
+//     DeleteLedger and BrokerCrash reset it to Nil (:158,:177);
+//   - a compacted ledger is Nil or CompactMessages(messages, Len(messages)):
+//     CompactorPhaseTwoWrite is its only writer and writes the messages up to
+//     phaseOneResult.readPosition = Len(messages) (:124-130); DeleteLedger
+//     resets one to Nil (:160-163);
+//   - compactionHorizon is 0 or Len(messages): UpdateHorizon copies
+//     readPosition (:143), BrokerCrash copies the cursor's horizon or 0
+//     (:178-180);
+//   - the cursor's horizon is 0 or Len(messages): PersistCursor copies
+//     compactionHorizon (:149).
+// So a component code keeps one bit per two-valued field and the other
+// fields as they are (LSB first):
+//
+//   P   C bits          ledger j present (j = 1..C)
+//   R   1               phaseOneResult = Len(messages) (else Nil)
+//   H   1               compactionHorizon = Len(messages) (else 0)
+//   ph  3               compactorState
+//   X   bits(C)         compactedTopicContext
+//   CP  1               cursor present
+//   CH  1               cursor horizon = Len(messages) (else 0)
+//   CC  bits(C)         cursor context
+//   CR  bits(K)         crashTimes
+//
+// The shipped constants (C = 3, K = 1) take 15 bits.  Every transition and
+// invariant below is component_model.h's on the decoded key (code_decode):
+// tlcg_host_component_selfcheck runs both on every state of whole components
+// and checks that each reachable local key encodes and decodes back to itself
+// (so the four facts above are checked, not assumed, on every golden cfg).
+// The kernel checks the initial state's round trip; a component whose initial
+// key does not encode goes to the 32-bit cascade pass.
+#pragma once
+#if !defined(__HIPCC_RTC__)
+#include "component_model.h"
+#endif
+
+namespace tlcg {
+
+typedef uint32_t ckey;  // component code
+
+// field offsets of a code (functions of the layout: constant-fold under hipRTC)
+TLCG_HD int cc_r(const Layout& L) { return L.C; }
+TLCG_HD int cc_h(const Layout& L) { return L.C + 1; }
+TLCG_HD int cc_ph(const Layout& L) { return L.C + 2; }
+TLCG_HD int cc_x(const Layout& L) { return L.C + 5; }
+TLCG_HD int cc_cp(const Layout& L) { return cc_x(L) + L.ctx_w; }
+TLCG_HD int cc_ch(const Layout& L) { return cc_cp(L) + 1; }
+TLCG_HD int cc_cc(const Layout& L) { return cc_ch(L) + 1; }
+TLCG_HD int cc_cr(const Layout& L) { return cc_cc(L) + L.curc_w; }
+TLCG_HD int code_bits(const Layout& L) { return cc_cr(L) + L.cr_w; }
+
+TLCG_HD uint32_t cget(ckey c, int sh, int w) { return (c >> sh) & lmask(w); }
+TLCG_HD ckey cset(ckey c, int sh, int w, uint32_t v) {
+  const ckey m = lmask(w) << sh;
+  return (c & ~m) | ((v << sh) & m);
+}
+
+// per-component constants: everything the code functions read besides the code
+struct CodeConsts {
+  uint32_t len;   // Len(messages)
+  lkey ledbits;   // a present ledger's local-key bits at ledger offset 0: 1 | CompactMessages(messages, len) << 1
+  int msgs_ok;    // TypeSafe's messages conjunct
+  int hz_live;    // CompactionHorizonCorrectness at horizon = len: some position is not skipped
+  int hz_false;   // ... and one of them has no witness in CompactMessages(messages, len)
+  int dn0, dn1;   // DuplicateNullKeyMessage is FALSE at horizon 0 / len (ledger present)
+};
+
+TLCG_HD CodeConsts code_consts(const Layout& L, const CompMsgs& c) {
+  CodeConsts k;
+  k.len = (uint32_t)c.len;
+  const u64 cm = (c.len >= 1 && c.len <= L.N) ? (c.cm >> ((c.len - 1) * L.N)) & nmask(L.N) : 0;
+  k.ledbits = (lkey)(1u | (cm << 1));
+  k.msgs_ok = c.msgs_ok;
+  const int hz = c.len <= L.N ? c.len : L.N;
+  const uint32_t live = (uint32_t)nmask(hz) & ~c.skip;
+  uint32_t fail = 0;
+  for (int i = 0; i < L.N; ++i) fail |= (uint32_t)((cm & ((c.need >> (i * L.N)) & nmask(L.N))) == 0) << i;
+  k.hz_live = live != 0;
+  k.hz_false = (fail & live) != 0;
+  const u64 upto = nmask(c.len < L.N ? c.len : L.N);
+  k.dn0 = (cm & c.null_pos & upto) != 0;
+  k.dn1 = (cm & c.null_pos & upto & ~nmask(c.len)) != 0;
+  return k;
+}
+
+// local key -> code (lossy off the reachable space: code_decode checks)
+TLCG_HD ckey code_encode(const Layout& L, lkey k) {
+  ckey c = 0;
+  for (int j = 1; j <= L.C; ++j) c |= (ckey)k_led_present(L, k, j) << (j - 1);
+  c |= (ckey)(k_p1r(L, k) != 0) << cc_r(L);
+  c |= (ckey)(k_hz(L, k) != 0) << cc_h(L);
+  c |= (ckey)k_phase(L, k) << cc_ph(L);
+  c |= (ckey)k_ctx(L, k) << cc_x(L);
+  c |= (ckey)k_cur_present(L, k) << cc_cp(L);
+  c |= (ckey)(k_cur_h(L, k) != 0) << cc_ch(L);
+  c |= (ckey)k_cur_c(L, k) << cc_cc(L);
+  c |= (ckey)k_crash(L, k) << cc_cr(L);
+  return c;
+}
+
+// code -> local key
+TLCG_HD lkey code_decode(const Layout& L, const CodeConsts& K, ckey c) {
+  lkey k = 0;
+  for (int j = 1; j <= L.C; ++j)
+    if ((c >> (j - 1)) & 1) k |= K.ledbits << k_led_off(L, j);
+  if ((c >> cc_r(L)) & 1) k = lset(L, k, L.p1r_sh, L.p1r_w, K.len);
+  k = lset(L, k, L.ph_sh, 3, cget(c, cc_ph(L), 3));
+  if ((c >> cc_h(L)) & 1) k = lset(L, k, L.hz_sh, L.hz_w, K.len);
+  k = lset(L, k, L.ctx_sh, L.ctx_w, cget(c, cc_x(L), L.ctx_w));
+  if ((c >> cc_cp(L)) & 1) {
+    const lkey h = ((c >> cc_ch(L)) & 1) ? K.len : 0u;
+    const lkey cur = 1u | (h << 1) | (cget(c, cc_cc(L), L.curc_w) << (1 + L.curh_w));
+    k = lset(L, k, L.cur_sh, 1 + L.curh_w + L.curc_w, cur);
+  }
+  k = lset(L, k, L.cr_sh, L.cr_w, cget(c, cc_cr(L), L.cr_w));
+  return k;
+}
+
+TLCG_HD int c_phase(const Layout& L, ckey c) { return (int)cget(c, cc_ph(L), 3); }
+// MaxCompactedLedgerId, compaction.tla:103-106
+TLCG_HD int c_max_ledger(const Layout& L, ckey c) {
+  const uint32_t p = c & lmask(L.C);
+  return p ? highbit32(p) + 1 : 0;
+}
+
+// The compactor disjunct, compaction.tla:93-165 (compactor_step_k on codes).
+// Returns 0 disabled, 1 enabled (*t, *act set), 2 evaluation error (*act set).
+TLCG_HD int compactor_step_c(const Layout& L, const CodeConsts& K, ckey c, int ph, ckey* t, int* act) {
+  const uint32_t r = (c >> cc_r(L)) & 1;
+  switch (ph) {
+    case PH_ONE:  // CompactorPhaseOne, :93-100: readPosition := Len(messages)
+      if (r || K.len == 0) return 0;
+      *t = cset(c | (1u << cc_r(L)), cc_ph(L), 3, PH_WRITE);
+      *act = ACT_PHASEONE;
+      return 1;
+    case PH_WRITE: {  // CompactorPhaseTwoWrite, :121-132: ledger MaxCompactedLedgerId + 1
+      if (!r) return 0;
+      const int nid = c_max_ledger(L, c) + 1;
+      if (nid > L.C) return 0;
+      *t = cset(c | (1u << (nid - 1)), cc_ph(L), 3, PH_UCTX);
+      *act = ACT_WRITE;
+      return 1;
+    }
+    case PH_UCTX:  // CompactorPhaseTwoUpdateContext, :135-139
+      *t = cset(cset(c, cc_x(L), L.ctx_w, (uint32_t)c_max_ledger(L, c)), cc_ph(L), 3, PH_UHOR);
+      *act = ACT_UCTX;
+      return 1;
+    case PH_UHOR:  // CompactorPhaseTwoUpdateHorizon, :141-145: horizon := readPosition
+      *act = ACT_UHOR;
+      if (!r) return 2;  // phaseOneResult.readPosition of Nil
+      *t = cset(c | (1u << cc_h(L)), cc_ph(L), 3, PH_PERSIST);
+      return 1;
+    case PH_PERSIST: {  // CompactorPhaseTwoPersistCusror, :147-151: cursor := [horizon, context]
+      ckey u = c | (1u << cc_cp(L));
+      u = cset(u, cc_ch(L), 1, (c >> cc_h(L)) & 1);
+      u = cset(u, cc_cc(L), L.curc_w, cget(c, cc_x(L), L.ctx_w));
+      *t = cset(u, cc_ph(L), 3, PH_DELETE);
+      *act = ACT_PERSIST;
+      return 1;
+    }
+    case PH_DELETE: {  // CompactorPhaseTwoDeleteLedger, :153-165
+      *act = ACT_DELETE;
+      const int m = c_max_ledger(L, c);
+      ckey u = cset(c & ~(1u << cc_r(L)), cc_ph(L), 3, PH_ONE);
+      if (m != 1) {  // oldCompactedLedgerId = m - 1 (Nil when m = 1)
+        if (m - 1 < 1) return 2;  // compactedLedgers[old] out of domain
+        u &= ~(1u << (m - 2));
+      }
+      *t = u;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+// BrokerCrash, compaction.tla:169-182.  Returns 1 if enabled.
+TLCG_HD int crash_step_c(const Layout& L, ckey c, ckey* t) {
+  const uint32_t cr = cget(c, cc_cr(L), L.cr_w);
+  if ((int)cr >= L.K) return 0;
+  ckey u = cset(c, cc_cr(L), L.cr_w, cr + 1);
+  u = cset(u & ~(1u << cc_r(L)), cc_ph(L), 3, PH_ONE);
+  const uint32_t cp = (c >> cc_cp(L)) & 1;
+  u = cset(u, cc_h(L), 1, cp ? (c >> cc_ch(L)) & 1 : 0u);
+  *t = cset(u, cc_x(L), L.ctx_w, cp ? cget(c, cc_cc(L), L.curc_w) : 0u);
+  return 1;
+}
+
+// Consumer (:185-186) when modelled, and Terminating (:205-214)
+TLCG_HD int selfloop_count_c(const Layout& L, const CodeConsts& K, ckey c) {
+  const int term = (int)K.len == L.N && L.term_ok && c_phase(L, c) == PH_WRITE && c_max_ledger(L, c) == L.C;
+  return (L.consumer ? 1 : 0) + term;
+}
+
+// TypeSafe, compaction.tla:236-248 (inv_typesafe_k on the decoded key)
+TLCG_HD int inv_typesafe_c(const Layout& L, const CodeConsts& K, ckey c) {
+  const uint32_t r = ((c >> cc_r(L)) & 1) ? K.len : 0u;
+  const uint32_t hz = ((c >> cc_h(L)) & 1) ? K.len : 0u;
+  const uint32_t h = ((c >> cc_ch(L)) & 1) ? K.len : 0u;
+  const int cc = (int)cget(c, cc_cc(L), L.curc_w);
+  const bool ok = K.msgs_ok & (r == 0 || r <= K.len) & (c_phase(L, c) <= PH_DELETE) & ((int)hz <= L.N) &
+                  ((int)cget(c, cc_x(L), L.ctx_w) <= L.C) & ((int)cget(c, cc_cr(L), L.cr_w) <= L.K) &
+                  (!((c >> cc_cp(L)) & 1) || (h >= 1 && (int)h <= L.N && cc >= 1 && cc <= L.C));
+  return ok ? EV_TRUE : EV_FALSE;
+}
+
+// CompactedLedgerLeak, compaction.tla:253
+TLCG_HD int inv_leak_c(const Layout& L, ckey c) { return popcount32(c & lmask(L.C)) <= 2 ? EV_TRUE : EV_FALSE; }
+
+// the ledger compactedTopicContext names exists (else evaluating it fails)
+TLCG_HD bool ctx_ledger_ok(const Layout& L, ckey c) {
+  const int ctx = (int)cget(c, cc_x(L), L.ctx_w);
+  return ctx >= 1 && ctx <= L.C && ((c >> (ctx - 1)) & 1);
+}
+
+// CompactionHorizonCorrectness, compaction.tla:259-274 (inv_horizon_k): the
+// horizon is 0 (holds) or Len(messages), where the context's ledger, when
+// present, holds CompactMessages(messages, Len(messages)) (CodeConsts)
+TLCG_HD int inv_horizon_c(const Layout& L, const CodeConsts& K, ckey c) {
+  if (!((c >> cc_h(L)) & 1) || K.len == 0) return EV_TRUE;
+  if (!K.hz_live) return EV_TRUE;
+  if (!ctx_ledger_ok(L, c)) return EV_ERROR;
+  return K.hz_false ? EV_FALSE : EV_TRUE;
+}
+
+// DuplicateNullKeyMessage, compaction.tla:280-294 (inv_dupnull_k)
+TLCG_HD int inv_dupnull_c(const Layout& L, const CodeConsts& K, ckey c) {
+  if (!(L.retain && cget(c, cc_x(L), L.ctx_w) != 0)) return EV_TRUE;
+  if (!ctx_ledger_ok(L, c)) return EV_ERROR;
+  return (((c >> cc_h(L)) & 1) ? K.dn1 : K.dn0) ? EV_FALSE : EV_TRUE;
+}
+
+// first failing invariant in cfg order: -1 all hold, else (index << 1) | is_error
+TLCG_HD int check_invariants_c(const Layout& L, const CodeConsts& K, ckey c) {
+  for (int q = 0; q < L.n_inv; ++q) {
+    int r;
+    switch (L.inv[q]) {
+      case INV_TYPESAFE: r = inv_typesafe_c(L, K, c); break;
+      case INV_LEAK: r = inv_leak_c(L, c); break;
+      case INV_HORIZON: r = inv_horizon_c(L, K, c); break;
+      case INV_DUPNULL: r = inv_dupnull_c(L, K, c); break;
+      default: r = EV_ERROR;
+    }
+    if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
+  }
+  return -1;
+}
+
+}  // namespace tlcg

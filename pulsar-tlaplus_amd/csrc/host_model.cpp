@@ -2,6 +2,7 @@
 // model-level (context-free) C-ABI entry points.
 #include "host_model.h"
 
+#include "component_code.h"
 #include "component_model.h"
 
 #include <algorithm>
@@ -394,7 +395,10 @@ int64_t tlcg_host_termination_counterexample(const tlcg_model* m) {
 // Component-specialized evaluators (component_model.h) vs the generic ones
 // (model.h) on every state of the components of initial states
 // [first, first + n): the compactor successor, the stutter count and the
-// first failing invariant must agree.  Returns the states compared, or
+// first failing invariant must agree.  The same for component codes
+// (component_code.h): every reachable local key must encode and decode back
+// to itself (the two-valued fields the code relies on), and the code
+// evaluators must decode to the same successors and results.  Returns the states compared, or
 // -(1 + index of the first disagreeing state) on a mismatch.
 int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint64_t n) {
   HostModel hm;
@@ -425,6 +429,19 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
       int a3 = -1;
       const int r3 = compactor_step_k_sel(L, cm, msgs, k, k_phase(L, k), &t3, &a3);  // the branch-free form
       if (r3 != r1 || a3 != a1 || (r1 == 1 && t3 != t2)) return -(1 + checked);
+      {  // component codes
+        const CodeConsts kc = code_consts(L, cm);
+        const ckey cd = code_encode(L, k);
+        ckey ct = 0, cx = 0;
+        int ca = -1;
+        const int rc = compactor_step_c(L, kc, cd, c_phase(L, cd), &ct, &ca);
+        const int xc = crash_step_c(L, cd, &cx);
+        if (code_decode(L, kc, cd) != k || rc != r1 || ca != a1 || (r1 == 1 && code_decode(L, kc, ct) != t2) ||
+            xc != x2 || (xc && code_decode(L, kc, cx) != c2) ||
+            check_invariants_c(L, kc, cd) != check_invariants_k(L, cm, k) ||
+            selfloop_count_c(L, kc, cd) != selfloop_count_k(L, cm, k))
+          return -(1 + checked);
+      }
       if (r1 != r2 || a1 != a2 || (r1 == 1 && t1 != (msgs | ((u64)t2 << mb))) || x1 != x2 ||
           (x1 && t2w != (msgs | ((u64)c2 << mb))) || check_invariants(L, s) != check_invariants_k(L, cm, k) ||
           selfloop_count(L, s) != selfloop_count_k(L, cm, k))

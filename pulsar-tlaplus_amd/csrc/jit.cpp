@@ -35,7 +35,7 @@ std::string layout_literal(const Layout& L) {
 }
 
 std::string program_source(const Layout& L) {
-  std::string s = "typedef unsigned char uint8_t; typedef unsigned int uint32_t; typedef int int32_t;\n"
+  std::string s = "typedef unsigned char uint8_t; typedef unsigned short uint16_t; typedef unsigned int uint32_t; typedef int int32_t;\n"
                   "typedef unsigned long uint64_t; typedef long int64_t;\n";
   // tuning experiments: TLCG_JIT_DEFINES="A=1;B" becomes #define lines (part of the cache key)
   if (const char* d = std::getenv("TLCG_JIT_DEFINES")) {
@@ -54,9 +54,14 @@ std::string program_source(const Layout& L) {
   s += "\n" + layout_literal(L);
   for (int K : {32, 64, 128, 255})
     for (const char* od : {"false", "true"})
-      s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_component_") +
-           (od[0] == 't' ? "od_" : "") + std::to_string(K) + "(tlcg::CompArgs a) { tlcg::component_body<" +
-           std::to_string(K) + ", " + od + ">(a, kL); }\n";
+      for (const char* code : {"false", "true"}) {
+        if (code[0] == 't' && K > 64) continue;
+        // tlcg_component{_,_od_,c_,cod_}K: c = component codes, od = outdegree counts
+        s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_component") +
+             (code[0] == 't' ? (od[0] == 't' ? "cod_" : "c_") : (od[0] == 't' ? "_od_" : "_")) + std::to_string(K) +
+             "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ", " + od + ", " + code +
+             ">(a, kL); }\n";
+      }
   return s;
 }
 
@@ -125,7 +130,7 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
   arch = arch.substr(0, arch.find(':'));
   const std::string src = program_source(L);
   char key[64];
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v1"));
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2"));
   const std::string dir = cache_dir();
   const std::string path = dir + "/" + key + "-" + arch + ".co";
   std::vector<char> code;
@@ -154,6 +159,13 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
         *err = "hipModuleGetFunction " + n;
         return false;
       }
+      if (i < 2) {
+        const std::string nc = std::string(od ? "tlcg_componentcod_" : "tlcg_componentc_") + names[i];
+        if (hipModuleGetFunction(od ? &out->code_od[i] : &out->code[i], out->module, nc.c_str()) != hipSuccess) {
+          *err = "hipModuleGetFunction " + nc;
+          return false;
+        }
+      }
     }
   return true;
 }
@@ -163,10 +175,11 @@ void jit_release(JitKernels* k) {
   if (k) *k = JitKernels();
 }
 
-bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, hipStream_t stream) {
+bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream) {
   if (!a.n_comp) return true;
   const int i = K == 32 ? 0 : K == 64 ? 1 : K == 128 ? 2 : 3;
   hipFunction_t f = a.outdeg ? k.component_od[i] : k.component[i];
+  if (code && i < 2) f = a.outdeg ? k.code_od[i] : k.code[i];
   const uint64_t batches = (a.n_comp + 63) / 64;
   const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
   CompArgs copy = a;

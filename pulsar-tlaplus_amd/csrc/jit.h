@@ -15,6 +15,8 @@ struct JitKernels {
   hipModule_t module = nullptr;
   hipFunction_t component[4] = {nullptr, nullptr, nullptr, nullptr};     // K = 32, 64, 128, 255
   hipFunction_t component_od[4] = {nullptr, nullptr, nullptr, nullptr};  // the same, counting outdegrees
+  hipFunction_t code[2] = {nullptr, nullptr};     // component codes (component_code.h), K = 32, 64
+  hipFunction_t code_od[2] = {nullptr, nullptr};
   double compile_s = 0;  // 0 when loaded from the cache
   bool cached = false;
 };
@@ -25,6 +27,6 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err);
 // compile only (no device needed): the code object for `arch`
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err);
 void jit_release(JitKernels* k);
-bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, hipStream_t stream);
+bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream);
 
 }  // namespace tlcg

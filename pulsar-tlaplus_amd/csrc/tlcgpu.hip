@@ -23,6 +23,7 @@
 #include <sys/mman.h>
 
 #include "component.h"
+#include "component_code.h"
 #include "exchange.h"
 #include "host_model.h"
 #include "jit.h"
@@ -840,6 +841,7 @@ struct tlcg_ctx {
   JitKernels jit;
   int jit_state = 0;
   bool jit_used = false;
+  bool comp_code = false;  // the component engine's first pass runs component codes
   std::string jit_error;
   u64 pending = 0;      // states appended to the current level, not yet committed
   // kernel variant (tuning; env TLCG_FAST_ITEMS / TLCG_PROBE / TLCG_GRID)
@@ -1556,7 +1558,7 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
                       : (depth ? c->level_base[(size_t)depth] - c->level_base[(size_t)depth - 1] : 0);
   st->depth = depth;
   st->engine = (uint64_t)c->engine;
-  st->jit_used = c->jit_used ? 1 : 0;
+  st->jit_used = (c->jit_used ? 1 : 0) | (c->engine == TLCG_ENGINE_COMPONENT && c->comp_code ? 2 : 0);
   st->host_states = c->win;
   st->fpset_host_states = c->t0_base;
   if (std::getenv("TLCG_TIER_TRACE") && c->opts.fpset_spill)
@@ -1783,6 +1785,8 @@ int run_component(tlcg_ctx* c) {
     if (c->jit_state < 0) c->jit_error = e;
   }
   c->jit_used = want_jit && c->jit_state == 1;
+  const char* cv = std::getenv("TLCG_CODE");  // 0: 32-bit local keys throughout (A/B)
+  c->comp_code = code_bits(L) <= 16 && !(cv && std::atoi(cv) == 0);
   // on-chip capacity cascade; the first step is tunable (TLCG_COMP_K0 = 32 / 64)
   int kCascade[4] = {64, 128, 255, 0};
   if (const char* k0 = std::getenv("TLCG_COMP_K0"))
@@ -1823,7 +1827,10 @@ int run_component(tlcg_ctx* c) {
     a.lvl_gen = c->d_comp + COMP_MAXLV + 7;
     a.ovf_list = c->d_ovf[out];
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
-    if (!(c->jit_used ? jit_launch_component(c->jit, a, K, c->stream) : launch_component(a, K, c->stream))) {
+    // the first pass runs component codes when they fit 16 bits (component_code.h);
+    // a component whose initial key is no code, and the cascade, run 32-bit keys
+    const bool code = p == 0 && K <= 64 && c->comp_code;
+    if (!(c->jit_used ? jit_launch_component(c->jit, a, K, code, c->stream) : launch_component(a, K, code, c->stream))) {
       c->err = "component kernel launch failed";
       return -1;
     }
