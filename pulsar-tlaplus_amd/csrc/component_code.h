@@ -181,6 +181,35 @@ TLCG_HD int compactor_step_c(const Layout& L, const CodeConsts& K, ckey c, int p
   return 0;
 }
 
+// The same disjunct without branches (the kernel's form): every phase's
+// successor is a few bit operations on the code, so all six are formed and
+// the one of compactorState selected; the phase after ph is ph + 1 (DELETE ->
+// ONE).  *act is set when the result is not 0, as compactor_step_c.
+TLCG_HD int compactor_step_cb(const Layout& L, const CodeConsts& K, ckey c, ckey* t, int* act) {
+  const uint32_t ph = cget(c, cc_ph(L), 3);
+  const uint32_t r = (c >> cc_r(L)) & 1, hb = (c >> cc_h(L)) & 1;
+  const int m = c_max_ledger(L, c);
+  const ckey base = c & ~(7u << cc_ph(L));
+  const ckey t_one = base | (1u << cc_r(L));                                   // :96-97
+  const ckey t_write = base | (m < L.C ? 1u << m : 0u);                        // :124-130, ledger m + 1
+  const ckey t_uctx = cset(base, cc_x(L), L.ctx_w, (uint32_t)m);               // :137
+  const ckey t_uhor = base | (1u << cc_h(L));                                  // :143
+  const ckey t_pers = cset(cset(base | (1u << cc_cp(L)), cc_ch(L), 1, hb), cc_cc(L), L.curc_w,
+                           cget(c, cc_x(L), L.ctx_w));                         // :149
+  const ckey t_del = base & ~(1u << cc_r(L)) & ~(m >= 2 ? 1u << (m - 2) : 0u);  // :156-163
+  ckey u = t_one;
+  int res = (!r && K.len > 0) ? 1 : 0;
+  if (ph == PH_WRITE) { u = t_write; res = (r && m < L.C) ? 1 : 0; }
+  if (ph == PH_UCTX) { u = t_uctx; res = 1; }
+  if (ph == PH_UHOR) { u = t_uhor; res = r ? 1 : 2; }
+  if (ph == PH_PERSIST) { u = t_pers; res = 1; }
+  if (ph == PH_DELETE) { u = t_del; res = m == 0 ? 2 : 1; }
+  if (ph > PH_DELETE) res = 0;
+  *t = u | ((ph >= PH_DELETE ? (uint32_t)PH_ONE : ph + 1) << cc_ph(L));
+  if (res) *act = ACT_PHASEONE + (int)ph;
+  return res;
+}
+
 // BrokerCrash, compaction.tla:169-182.  Returns 1 if enabled.
 TLCG_HD int crash_step_c(const Layout& L, ckey c, ckey* t) {
   const uint32_t cr = cget(c, cc_cr(L), L.cr_w);
@@ -251,6 +280,26 @@ TLCG_HD int check_invariants_c(const Layout& L, const CodeConsts& K, ckey c) {
     if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
   }
   return -1;
+}
+
+// the same without branches (the kernel's form): every invariant's outcome
+// formed, then the first failing one in cfg order selected
+TLCG_HD int check_invariants_cb(const Layout& L, const CodeConsts& K, ckey c) {
+  const uint32_t hb = (c >> cc_h(L)) & 1;
+  const uint32_t X = cget(c, cc_x(L), L.ctx_w);
+  const bool ctx_ok = X >= 1 && (int)X <= L.C && ((c >> (X - 1)) & 1);
+  const int horizon = (!hb || K.len == 0 || !K.hz_live) ? EV_TRUE : !ctx_ok ? EV_ERROR : K.hz_false ? EV_FALSE : EV_TRUE;
+  const int dupnull = !(L.retain && X != 0) ? EV_TRUE : !ctx_ok ? EV_ERROR : (hb ? K.dn1 : K.dn0) ? EV_FALSE : EV_TRUE;
+  int res = -1;
+  for (int q = L.n_inv - 1; q >= 0; --q) {
+    int r = EV_ERROR;
+    if (L.inv[q] == INV_TYPESAFE) r = inv_typesafe_c(L, K, c);
+    if (L.inv[q] == INV_LEAK) r = inv_leak_c(L, c);
+    if (L.inv[q] == INV_HORIZON) r = horizon;
+    if (L.inv[q] == INV_DUPNULL) r = dupnull;
+    if (r != EV_TRUE) res = (q << 1) | (r == EV_ERROR ? 1 : 0);
+  }
+  return res;
 }
 
 }  // namespace tlcg

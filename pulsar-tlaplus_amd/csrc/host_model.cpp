@@ -412,6 +412,19 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
     const u64 s0 = init_state(L, idx);
     const u64 msgs = s0 & L.msgs_mask;
     const CompMsgs cm = comp_msgs_init(L, s0);
+    if (idx < first + 16 && code_bits(L) <= 16) {
+      // the kernel's branch-free code functions vs the branching ones on every
+      // code of the first components, reachable or not
+      const CodeConsts kc = code_consts(L, cm);
+      for (ckey cd = 0; cd < (1u << code_bits(L)); ++cd) {
+        ckey t1 = 0, t2 = 0;
+        int a1 = -1, a2 = -1;
+        const int r1 = compactor_step_c(L, kc, cd, c_phase(L, cd), &t1, &a1);
+        const int r2 = compactor_step_cb(L, kc, cd, &t2, &a2);
+        if (r1 != r2 || a1 != a2 || (r1 == 1 && t1 != t2) || check_invariants_c(L, kc, cd) != check_invariants_cb(L, kc, cd))
+          return -(1 + checked);
+      }
+    }
     std::unordered_set<u64> seen{s0};
     std::vector<u64> todo{s0};
     while (!todo.empty()) {
