@@ -99,7 +99,8 @@ typedef struct tlcg_opts {
   int32_t tlc_order;         /* 1: order every level like TLC -workers 1 (exact TLC trace) */
   int32_t rank, world;       /* fingerprint partition: this context owns rank of world */
   int32_t partition;         /* 0 auto (by `messages` when it is immutable), 1 by `messages`, 2 whole state */
-  int32_t engine;            /* TLCG_ENGINE_*: 0 auto, 1 global HBM FPSet, 2 component (closed partitions) */
+  int32_t engine;            /* TLCG_ENGINE_*: 0 auto, 1 global HBM FPSet, 2 component (closed partitions),
+                                3 component tree (Producer modelled) */
   /* Global engine: move committed levels other than the frontier (states and
    * parent log, the trace) to pinned host memory instead of growing the
    * device state store past device_store_cap states (0: past what free HBM
@@ -126,7 +127,9 @@ typedef struct tlcg_opts {
  * initial message sequence spans an independent component; a wavefront lane
  * runs TLC's FIFO BFS on one component with an on-chip FPSet.  Same counts,
  * same TLC-order trace; used by AUTO when every component fits on chip. */
-enum { TLCG_ENGINE_AUTO = 0, TLCG_ENGINE_GLOBAL = 1, TLCG_ENGINE_COMPONENT = 2 };
+enum { TLCG_ENGINE_AUTO = 0, TLCG_ENGINE_GLOBAL = 1, TLCG_ENGINE_COMPONENT = 2,
+       TLCG_ENGINE_TREE = 3 /* the component tree of a Producer-modelled spec (auto picks it; falls back to
+                               the global engine on an error to report or a component past 1024 states) */ };
 
 typedef struct tlcg_stats {
   uint64_t generated;        /* "states generated" (initial states included) */

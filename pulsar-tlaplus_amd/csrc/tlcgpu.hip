@@ -24,6 +24,7 @@
 
 #include "component.h"
 #include "component_code.h"
+#include "tree.h"
 #include "exchange.h"
 #include "host_model.h"
 #include "jit.h"
@@ -842,6 +843,13 @@ struct tlcg_ctx {
   int jit_state = 0;
   bool jit_used = false;
   bool comp_code = false;  // the component engine's first pass runs component codes
+  // component-tree engine (tree.h): depths and sizes of every component's chunk, counters
+  uint8_t* d_tree_dep = nullptr;
+  uint32_t* d_tree_n = nullptr;
+  u64 tree_slots = 0, tree_comps = 0;  // capacities of the two arrays
+  unsigned long long* d_tree_ctr = nullptr;  // lvl[TREE_MAXLV], lvl_gen[TREE_MAXLV], flags
+  unsigned long long* h_tree_ctr = nullptr;
+  int tree_cap = 0;  // slots per component of the last tree run (0: none)
   std::string jit_error;
   u64 pending = 0;      // states appended to the current level, not yet committed
   // kernel variant (tuning; env TLCG_FAST_ITEMS / TLCG_PROBE / TLCG_GRID)
@@ -949,7 +957,7 @@ const tlcg_ctx::HostChunk& chunk_of(const tlcg_ctx* c, u64 g) {
 
 // first unused slot of the state store
 u64 store_end(const tlcg_ctx* c) {
-  return c->engine == TLCG_ENGINE_COMPONENT ? c->comp_store_used : distinct_of(c);
+  return c->engine != TLCG_ENGINE_GLOBAL ? c->comp_store_used : distinct_of(c);
 }
 
 // Pinned host memory for spilled levels.  hipHostMalloc pins 4 KiB pages one
@@ -1548,7 +1556,7 @@ bool read_ctr(tlcg_ctx* c) {
 void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   if (!st) return;
   std::memset(st, 0, sizeof *st);
-  const bool comp = c->engine == TLCG_ENGINE_COMPONENT;
+  const bool comp = c->engine != TLCG_ENGINE_GLOBAL;  // an on-chip engine (component, tree)
   const u64 d = comp ? c->comp_distinct : distinct_of(c);
   const int depth = comp ? (int)c->comp_levels.size()
                          : (c->level_base.empty() ? 0 : (int)c->level_base.size() - 1);
@@ -1876,6 +1884,123 @@ int run_component(tlcg_ctx* c) {
   return 1;
 }
 
+// ---- component-tree engine (tree.h) ----
+
+// applicable: Producer modelled (the component tree), one rank, one-word
+// states, local keys < 32 bits, no TLC order (its lanes do not keep TLC's
+// order) and no outdegree statistics (they need TLC's first discoverers);
+// TLCG_TREE=0 turns it off (A/B)
+bool tree_applicable(const tlcg_ctx* c) {
+  const Layout& L = c->hm.L;
+  const int mb = L.msg_sh + L.N * L.mw;
+  const char* tv = std::getenv("TLCG_TREE");
+  return L.producer && !(tv && std::atoi(tv) == 0) && !c->opts.tlc_order && c->opts.world == 1 && c->words == 1 &&
+         L.bits - mb <= 31 && L.N >= 1 && L.N <= 8 && !c->opts.outdegree && L.nkv >= 1 && c->hm.n_init >= 1;
+}
+
+// Run every layer of the component tree.  Returns 1 done, 0 the global
+// engine takes the model (an event to report as TLC does, a component past
+// 1024 states or TREE_MAXLV depths, or not enough memory), -1 error.
+int run_tree(tlcg_ctx* c) {
+  const Layout& L = c->hm.L;
+  std::vector<u64> ncomp(1, 1);  // components per layer: nkv^l
+  for (int l = 1; l <= L.N; ++l) {
+    if (ncomp.back() > (1ull << 34) / (u64)L.nkv) return 0;
+    ncomp.push_back(ncomp.back() * (u64)L.nkv);
+  }
+  u64 comps = 0;
+  for (u64 x : ncomp) comps += x;
+  if (!c->d_tree_ctr) {
+    const size_t bytes = sizeof(unsigned long long) * (2 * TREE_MAXLV + 1);
+    if (!alloc_bytes(c, (void**)&c->d_tree_ctr, bytes, "tree counters")) return -1;
+    HIPCHK_I(hipHostMalloc((void**)&c->h_tree_ctr, bytes));
+  }
+  for (int cap : {512, 1024}) {
+    const u64 slots = comps * (u64)cap;
+    // the store (state + parent), the depth bytes and the sizes must fit next to what is allocated
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+    const double have = (double)fr + 16.0 * (double)c->cap + (double)c->tree_slots + 4.0 * (double)c->tree_comps;
+    if (17.0 * (double)slots + 4.0 * (double)comps > 0.85 * have) return 0;
+    c->engine = TLCG_ENGINE_TREE;
+    c->comp_store_used = 0;  // nothing of an earlier run to keep (tlcg_init freed the host chunks)
+    if (!ensure_store(c, slots)) return -1;
+    if (c->tree_slots < slots) {
+      hipFree(c->d_tree_dep);
+      c->d_tree_dep = nullptr;
+      c->tree_slots = 0;
+      if (!alloc_bytes(c, (void**)&c->d_tree_dep, slots, "tree depths")) return -1;
+      c->tree_slots = slots;
+    }
+    if (c->tree_comps < comps) {
+      hipFree(c->d_tree_n);
+      c->d_tree_n = nullptr;
+      c->tree_comps = 0;
+      if (!alloc_bytes(c, (void**)&c->d_tree_n, comps * 4, "tree sizes")) return -1;
+      c->tree_comps = comps;
+    }
+    unsigned long long* ctr = c->d_tree_ctr;
+    HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * (2 * TREE_MAXLV + 1), c->stream));
+    HIPCHK_I(hipEventRecord(c->e0, c->stream));
+    u64 gbase = 0, cbase = 0, pgbase = 0, pcbase = 0;
+    for (int l = 0; l <= L.N; ++l) {
+      TreeArgs a;
+      a.L = L;
+      a.layer = l;
+      a.n_comp = ncomp[(size_t)l];
+      a.n_init = c->hm.n_init;
+      a.par_states = l ? c->d_states + pgbase : nullptr;
+      a.par_dep = l ? c->d_tree_dep + pgbase : nullptr;
+      a.par_n = l ? c->d_tree_n + pcbase : nullptr;
+      a.par_gbase = pgbase;
+      a.states = c->d_states + gbase;
+      a.parents = c->d_parents + gbase;
+      a.dep = c->d_tree_dep + gbase;
+      a.n_out = c->d_tree_n + cbase;
+      a.gbase = gbase;
+      a.rank_tag = (u64)c->opts.rank << 56;
+      a.lvl = ctr;
+      a.lvl_gen = ctr + TREE_MAXLV;
+      a.flags = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV);
+      if (!launch_tree(a, cap, c->stream)) {
+        c->err = "component-tree kernel launch failed";
+        return -1;
+      }
+      pgbase = gbase;
+      pcbase = cbase;
+      gbase += a.n_comp * (u64)cap;
+      cbase += a.n_comp;
+    }
+    HIPCHK_I(hipEventRecord(c->e1, c->stream));
+    HIPCHK_I(hipMemcpyAsync(c->h_tree_ctr, ctr, sizeof(unsigned long long) * (2 * TREE_MAXLV + 1),
+                            hipMemcpyDeviceToHost, c->stream));
+    HIPCHK_I(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->e0, c->e1);
+    c->kernel_ms += ms;
+    c->expand_ms += ms;
+    const unsigned flags = (unsigned)c->h_tree_ctr[2 * TREE_MAXLV];
+    if (flags & TREE_EVENT) return 0;  // the global engine finds TLC's first error and its trace
+    if (flags & TREE_OVERFLOW) continue;
+    c->tree_cap = cap;
+    c->passes.clear();
+    c->comp_levels.assign(c->h_tree_ctr, c->h_tree_ctr + TREE_MAXLV);
+    c->comp_level_gen.assign(c->h_tree_ctr + TREE_MAXLV, c->h_tree_ctr + 2 * TREE_MAXLV);
+    while (!c->comp_levels.empty() && c->comp_levels.back() == 0) c->comp_levels.pop_back();
+    c->comp_init = c->hm.n_init;
+    c->comp_distinct = 0;
+    for (u64 x : c->comp_levels) c->comp_distinct += x;
+    c->comp_generated = c->comp_init;
+    for (u64 x : c->comp_level_gen) c->comp_generated += x;
+    c->comp_store_used = slots;
+    c->outdeg_valid = false;
+    c->pending = 0;
+    c->status = TLCG_DONE;
+    return 1;
+  }
+  return 0;  // a component past 1024 states
+}
+
 bool run_init(tlcg_ctx* c) {
   c->engine = TLCG_ENGINE_GLOBAL;
   const HostModel& hm = c->hm;
@@ -2187,6 +2312,12 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
     *out = c;
     return -2;
   }
+  if (c->opts.engine == TLCG_ENGINE_TREE && !tree_applicable(c)) {
+    c->err = "the component-tree engine needs a modelled Producer, one rank, <= 63-bit states, no TLC-order "
+             "mode and no outdegree statistics";
+    *out = c;
+    return -2;
+  }
   if (c->opts.engine == TLCG_ENGINE_COMPONENT && !component_applicable(c)) {
     c->err = "the component engine needs an immutable `messages` (no Producer), no TLC-order mode and a closed partition";
     *out = c;
@@ -2249,6 +2380,10 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_aux);
   jit_release(&c->jit);
   hipFree(c->d_comp);
+  hipFree(c->d_tree_dep);
+  hipFree(c->d_tree_n);
+  hipFree(c->d_tree_ctr);
+  if (c->h_tree_ctr) hipHostFree(c->h_tree_ctr);
   hipFree(c->d_runs);
   hipFree(c->d_ovf[0]);
   hipFree(c->d_ovf[1]);
@@ -2277,6 +2412,17 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
   c->ev_level = -1;
   c->ev_parent_gidx = NO_PARENT;
   c->ev_action = -1;
+  if ((c->opts.engine == TLCG_ENGINE_AUTO || c->opts.engine == TLCG_ENGINE_TREE) && tree_applicable(c)) {
+    // the component-tree engine runs the whole BFS here; 0 = the global engine
+    // takes the model (an error to report, a component past the capacity, memory)
+    const int r = run_tree(c);
+    if (r < 0) return -10;
+    if (r == 1) {
+      c->inited = true;
+      fill_stats(c, st);
+      return 0;
+    }
+  }
   if (c->opts.engine != TLCG_ENGINE_GLOBAL && component_applicable(c)) {
     // the component engine runs the whole BFS here; 0 = a component needs the global engine
     const int r = run_component(c);
@@ -2300,7 +2446,7 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
 int tlcg_step_level(tlcg_ctx* c, tlcg_stats* st) {
   const DeviceGuard dg(c);
   if (!c || !c->inited) return -1;
-  if (c->engine == TLCG_ENGINE_COMPONENT) {  // the run finished in tlcg_init
+  if (c->engine != TLCG_ENGINE_GLOBAL) {  // the on-chip engines finish the run in tlcg_init
     fill_stats(c, st);
     return 0;
   }
@@ -2326,7 +2472,7 @@ int tlcg_run(tlcg_ctx* c, tlcg_stats* st) {
 
 int tlcg_level_sizes(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
   if (!c) return -1;
-  if (c->engine == TLCG_ENGINE_COMPONENT) {
+  if (c->engine != TLCG_ENGINE_GLOBAL) {
     const int depth = (int)c->comp_levels.size();
     for (int i = 0; i < depth && i < cap; ++i) out[i] = c->comp_levels[(size_t)i];
     if (n) *n = depth;
@@ -2543,7 +2689,7 @@ int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, ui
 int tlcg_level_generated(tlcg_ctx* c, uint64_t* out, int32_t cap, int32_t* n) {
   if (!c || !n) return -1;
   std::vector<u64> v;
-  if (c->engine == TLCG_ENGINE_COMPONENT) {
+  if (c->engine != TLCG_ENGINE_GLOBAL) {
     if (c->comp_levels.empty()) {
       *n = 0;
       return 0;
@@ -2661,7 +2807,7 @@ int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
     return -2;
   }
   if (c->engine != TLCG_ENGINE_GLOBAL) {
-    c->err = "the component engine completes the whole check inside tlcg_init: nothing to checkpoint";
+    c->err = "the on-chip engines complete the whole check inside tlcg_init: nothing to checkpoint";
     return -2;
   }
   if (c->pending || (c->status != TLCG_RUNNING && c->status != TLCG_DONE)) {

@@ -26,8 +26,8 @@ ACTIONS = ("Producer", "CompactorPhaseOne", "CompactorPhaseTwoWrite", "Compactor
            "CompactorPhaseTwoUpdateHorizon", "CompactorPhaseTwoPersistCusror", "CompactorPhaseTwoDeleteLedger",
            "BrokerCrash", "Consumer", "Terminating")
 STATUS = {0: "running", 1: "ok", 2: "invariant", 3: "deadlock", 4: "action_error", 5: "invariant_error"}
-ENGINES = {"auto": 0, "global": 1, "component": 2}
-ENGINE_NAMES = {1: "global", 2: "component"}
+ENGINES = {"auto": 0, "global": 1, "component": 2, "tree": 3}
+ENGINE_NAMES = {1: "global", 2: "component", 3: "tree"}
 
 
 class tlcg_model(C.Structure):

@@ -290,15 +290,17 @@ def test_g9deep_scaled_counts():
 
 
 
-def test_p8_producer_scaled_matches_oracle():
-    """An open (producer-modelled) state space of ~1e8 states on the global
-    engine: KeySpace = ValueSpace = 1..7, ModelProducer, RetainNullKey FALSE;
-    counts and every level against the C oracle (tests/golden/p8.json)."""
+@pytest.mark.parametrize("engine", ["auto", "global"])
+def test_p8_producer_scaled_matches_oracle(engine):
+    """An open (producer-modelled) state space of ~1e8 states on the
+    component-tree engine (auto) and on the global engine: KeySpace =
+    ValueSpace = 1..7, ModelProducer, RetainNullKey FALSE; counts and every
+    level against the C oracle (tests/golden/p8.json)."""
     import json
     import os
     g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "p8.json")))
-    r = tlcgpu.run(model_of(g["constants"]))
+    r = tlcgpu.run(model_of(g["constants"]), engine=engine)
     want = g["result"]
-    assert r.engine == "global" and r.status == "ok"
+    assert r.engine == ("tree" if engine == "auto" else "global") and r.status == "ok"
     assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
                                                             want["levels"])

@@ -1,0 +1,112 @@
+"""GPU: the component-tree engine (csrc/tree.hip; Producer modelled, the
+states of one `messages` value form a component and the components a tree
+by prefix, compaction.tla:83-87) against the golden fixtures and the ~1e8
+producer oracle run: counts, every level, depth and the generated counts
+per level; the parent log it writes walks back to Init through real
+successors; an error to report falls back to the global engine."""
+import json
+import os
+import ctypes as C
+import random
+
+import pytest
+
+import tlcgpu
+from conftest import FULL_CASES, GOLDEN, model_of
+
+pytestmark = pytest.mark.gpu
+
+PRODUCER_CASES = [c for c in FULL_CASES if GOLDEN[c]["constants"]["producer"]]
+OK_CASES = [c for c in PRODUCER_CASES if GOLDEN[c]["result"]["result"] == "ok"]
+ERR_CASES = [c for c in PRODUCER_CASES if GOLDEN[c]["result"]["result"] != "ok"]
+
+
+def test_there_are_producer_cases():
+    assert OK_CASES and ERR_CASES
+
+
+@pytest.mark.parametrize("case", OK_CASES)
+def test_tree_matches_golden(case):
+    m = model_of(GOLDEN[case]["constants"])
+    want = GOLDEN[case]["result"]
+    ck = tlcgpu.Checker(m)  # auto: the tree for <= 63-bit states, else the global engine
+    try:
+        r = ck.run()
+        assert r.engine == ("tree" if tlcgpu.state_words(m) == 1 else "global")
+        assert (r.status, r.generated, r.distinct, r.depth) == ("ok", want["generated"], want["distinct"], want["depth"])
+        assert r.levels == want["levels"]
+        # generated per level: the initial states, then each level's expansion, summing to the total
+        g = ck.level_generated()
+        assert len(g) == r.depth + 1 and sum(g) == r.generated
+        # the same numbers as the global engine, level by level
+        ref = tlcgpu.Checker(m, engine="global")
+        try:
+            ref.run()
+            assert ref.level_generated() == g
+        finally:
+            ref.close()
+    finally:
+        ck.close()
+
+
+@pytest.mark.parametrize("case", ["P_published"])
+def test_tree_parent_log_walks_to_init(case):
+    """Sampled stored states (positions < 60 of random components of layers
+    >= 1: every component there holds at least 62 states): each one's parent
+    reference names a stored state that has it as a successor, and every chain
+    ends at the initial state within the search depth."""
+    c = GOLDEN[case]["constants"]
+    m = model_of(c)
+    nkv = (len(c["keys"]) + 1) * (len(c["values"]) + 1)
+    cap = 512
+    ck = tlcgpu.Checker(m, engine="tree")
+    try:
+        r = ck.run(with_trace=False)
+        assert r.engine == "tree"
+        ob = tlcgpu.load_library().tlcg_ordinal_bits(C.byref(m.to_c()))
+        rng = random.Random(7)
+        base, layers = cap, []  # layer 0 is one chunk
+        for l in range(1, c["N"] + 1):
+            layers.append((base, nkv ** l))
+            base += nkv ** l * cap
+        for _ in range(300):
+            b0, n = rng.choice(layers)
+            g = b0 + rng.randrange(n) * cap + rng.randrange(60)
+            s, p = ck.state_at(g)
+            steps = 0
+            while p != (1 << 64) - 1:
+                ps, pp = ck.state_at((p & ((1 << 56) - 1)) >> ob)
+                assert s in [t for _, t in tlcgpu.host_successors(m, ps)], (case, g)
+                s, p = ps, pp
+                steps += 1
+                assert steps < r.depth
+            assert s == tlcgpu.host_init_state(m, 0)
+    finally:
+        ck.close()
+
+
+@pytest.mark.parametrize("case", ERR_CASES)
+def test_tree_error_falls_back_to_global(case):
+    m = model_of(GOLDEN[case]["constants"])
+    want = GOLDEN[case]["result"]
+    r = tlcgpu.run(m)  # auto: the tree finds the error, the global engine reports it
+    assert r.engine == "global"
+    assert r.status == want["result"] and r.depth == want["depth"]
+    assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+
+
+def test_p8_on_the_tree():
+    """~1e8 producer-modelled states (tests/golden/p8.json, from the C oracle)."""
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "p8.json")))
+    ck = tlcgpu.Checker(model_of(g["constants"]), engine="tree")
+    try:
+        r = ck.run()
+        want = g["result"]
+        assert r.engine == "tree"
+        assert (r.generated, r.distinct, r.depth) == (want["generated"], want["distinct"], want["depth"])
+        assert r.levels == want["levels"]
+        # a second check on the same context gives the same numbers
+        r2 = ck.run()
+        assert (r2.generated, r2.distinct, r2.levels) == (r.generated, r.distinct, r.levels)
+    finally:
+        ck.close()
