@@ -42,6 +42,7 @@ BYTES_PER_STATE_WORD = 8
 PMC_PROFILE = "pmc_k_expand.json"
 PMC_COMPONENT_PROFILE = "pmc_component.json"
 COMPONENT_BYTES_PER_STATE = 16  # state word + parent entry written to the HBM store
+TREE_BYTES_PER_STATE = 17       # the same + the state's depth byte (read back by the next layer)
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
 # algorithmic HBM bytes per distinct state of the BFS path (read
 # the frontier state 8 B, write the new state 8 B and its parent entry 8 B,
@@ -188,7 +189,7 @@ def main():
     import tlcgpu
 
     # a collective that does not complete (a peer rank died) aborts instead of hanging
-    os.environ.setdefault("TLCG_COMM_TIMEOUT_S", "180")
+    os.environ.setdefault("TLCG_COMM_TIMEOUT_S", "60")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -237,7 +238,7 @@ def main():
         counts = [st.generated, st.distinct]
         used = tlcgpu.ENGINE_NAMES.get(int(st.engine), "?")
         jit = int(st.jit_used)
-        launches = len(eng.level_sizes()) if used == "global" else 1
+        launches = len(eng.level_sizes()) if used == "global" else cfg.get("N", 3) + 1 if used == "tree" else 1
         if distributed:
             t = torch.tensor([elapsed, ems, kms], dtype=torch.float64, device=rdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -299,7 +300,7 @@ def main():
         main_run = time_exchange(0)  # successors leave their rank: the exchange is the path
     else:
         main_run = time_engine("auto")
-        global_run = time_engine("global") if not open_model else None
+        global_run = time_engine("global")  # the HBM-FPSet engine beside the on-chip one
         if distributed and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
             # a secondary measurement: its failure (every rank learns of it
             # through torch's own group) must not cost the headline line
@@ -393,11 +394,26 @@ def main():
                         "SQ_LDS_IDX_ACTIVE / 256 CU) / 2.4 GHz / kernel time (DESIGN 4)")
         return rf
 
+    def roofline_tree(r):
+        # SURVEY 8(d)'s per-unit figure x the distinct states of one step; the
+        # kernel writes 17 B/state (state, parent entry, depth byte) and reads
+        # 9 B per entry (its parent state and depth); its FPSets stay in LDS
+        bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
+        achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
+        return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                    kernel="k_tree<512> (component tree, one wavefront per messages value)",
+                    launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
+                    bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, kernel_bytes_per_distinct=TREE_BYTES_PER_STATE,
+                    kernel_written_gbs=round(TREE_BYTES_PER_STATE * distinct / world / (r["expand_ms"] * 1e-3) / 1e9,
+                                             1))
+
     def summary(r):
         out = dict(engine=r["engine"], jit=bool(r["jit"]), value=round(distinct * args.steps / r["elapsed"], 1),
                    ms_per_step=round(r["elapsed"] * 1e3 / args.steps, 3),
                    gpu_kernel_ms_per_step=round(r["kernel_ms"], 3),
-                   roofline=roofline_component(r) if r["engine"] == "component" else roofline_global(r))
+                   roofline=roofline_component(r) if r["engine"] == "component" else
+                   roofline_tree(r) if r["engine"] == "tree" else roofline_global(r))
         for k in ("partition", "exchange"):
             if k in r:
                 out[k] = r[k]
