@@ -27,8 +27,8 @@ CONFIGS = {
     "s": dict(keys=2, distinct=45_198, generated=60_507, depth=20),
     # CompactionTimesLimit = 12, a 93-bit (two-word) state
     "g9deep": dict(keys=10, C=12, distinct=986_759_477, generated=1_119_626_552, depth=74),
-    # an open state space: the producer modelled (no components; every level
-    # crosses ranks at N > 1), oracle-pinned in tests/golden/p8.json
+    # an open state space: the producer modelled (the component tree on one
+    # GPU; at N > 1 every level crosses ranks), oracle-pinned in tests/golden/p8.json
     "p8": dict(keys=7, producer=True, retain=False, distinct=91_781_506, generated=161_341_378, depth=23),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
