@@ -1888,14 +1888,17 @@ int run_component(tlcg_ctx* c) {
 
 // applicable: Producer modelled (the component tree), one rank, one-word
 // states, local keys < 32 bits, no TLC order (its lanes do not keep TLC's
-// order) and no outdegree statistics (they need TLC's first discoverers);
-// TLCG_TREE=0 turns it off (A/B)
+// order), no outdegree statistics (they need TLC's first discoverers), no
+// explicit device-store budget and no host FPSet tier (the tree keeps its
+// whole store on the device: a run that must spill takes the global
+// engine); TLCG_TREE=0 turns it off (A/B)
 bool tree_applicable(const tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   const int mb = L.msg_sh + L.N * L.mw;
   const char* tv = std::getenv("TLCG_TREE");
   return L.producer && !(tv && std::atoi(tv) == 0) && !c->opts.tlc_order && c->opts.world == 1 && c->words == 1 &&
-         L.bits - mb <= 31 && L.N >= 1 && L.N <= 8 && !c->opts.outdegree && L.nkv >= 1 && c->hm.n_init >= 1;
+         L.bits - mb <= 31 && L.N >= 1 && L.N <= 8 && !c->opts.outdegree && L.nkv >= 1 && c->hm.n_init >= 1 &&
+         !c->opts.device_store_cap && !c->opts.fpset_spill;
 }
 
 // Run every layer of the component tree.  Returns 1 done, 0 the global
@@ -2807,7 +2810,8 @@ int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
     return -2;
   }
   if (c->engine != TLCG_ENGINE_GLOBAL) {
-    c->err = "the on-chip engines complete the whole check inside tlcg_init: nothing to checkpoint";
+    c->err = "the on-chip engines (component engine, component tree) complete the whole check inside tlcg_init: "
+             "nothing to checkpoint";
     return -2;
   }
   if (c->pending || (c->status != TLCG_RUNNING && c->status != TLCG_DONE)) {

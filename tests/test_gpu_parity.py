@@ -189,7 +189,7 @@ def test_g9_scaled_counts_and_parent_log():
 def test_growth_and_redo_paths():
     # a 2^10-slot FPSet and a tiny store force FPSet/store growth and level redo
     m = model_of(GOLDEN["P_published"]["constants"])
-    ck = tlcgpu.Checker(m, log2_fpset_slots=10, state_capacity=1000)
+    ck = tlcgpu.Checker(m, log2_fpset_slots=10, state_capacity=1000, engine="global")
     try:
         r = ck.run()
         check_against_golden("P_published", r, False)
