@@ -17,7 +17,8 @@
 //     (:178-180);
 //   - the cursor's horizon is 0 or Len(messages): PersistCursor copies
 //     compactionHorizon (:149).
-// So a component code keeps one bit per two-valued field and the other
+// (SURVEY App.A.1 derives the same facts by hand.)  So a component code keeps
+// one bit per two-valued field and the other
 // fields as they are (LSB first):
 //
 //   P   C bits          ledger j present (j = 1..C)

@@ -1901,9 +1901,11 @@ bool tree_applicable(const tlcg_ctx* c) {
          !c->opts.device_store_cap && !c->opts.fpset_spill;
 }
 
-// Run every layer of the component tree.  Returns 1 done, 0 the global
-// engine takes the model (an event to report as TLC does, a component past
-// 1024 states or TREE_MAXLV depths, or not enough memory), -1 error.
+// Run every layer of the component tree: chunks of 384 states per component
+// (the shipped N = 3, C = 3, K = 1 have at most 359), then 1024 if one
+// overflows.  Returns 1 done, 0 the global engine takes the model (an event
+// to report as TLC does, a component past 1024 states or TREE_MAXLV depths,
+// or not enough memory), -1 error.
 int run_tree(tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   std::vector<u64> ncomp(1, 1);  // components per layer: nkv^l
@@ -1914,11 +1916,14 @@ int run_tree(tlcg_ctx* c) {
   u64 comps = 0;
   for (u64 x : ncomp) comps += x;
   if (!c->d_tree_ctr) {
-    const size_t bytes = sizeof(unsigned long long) * (2 * TREE_MAXLV + 1);
+    const size_t bytes = sizeof(unsigned long long) * (2 * TREE_MAXLV + 2);
     if (!alloc_bytes(c, (void**)&c->d_tree_ctr, bytes, "tree counters")) return -1;
     HIPCHK_I(hipHostMalloc((void**)&c->h_tree_ctr, bytes));
   }
-  for (int cap : {512, 1024}) {
+  // components per wavefront (tuning hook TLCG_TREE_G = 1 / 2 / 4)
+  int groups = 4;
+  if (const char* gv = std::getenv("TLCG_TREE_G")) groups = std::atoi(gv) == 1 ? 1 : std::atoi(gv) == 2 ? 2 : 4;
+  for (int cap : {384, 1024}) {
     const u64 slots = comps * (u64)cap;
     // the store (state + parent), the depth bytes and the sizes must fit next to what is allocated
     size_t fr = 0, tot = 0;
@@ -1943,7 +1948,7 @@ int run_tree(tlcg_ctx* c) {
       c->tree_comps = comps;
     }
     unsigned long long* ctr = c->d_tree_ctr;
-    HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * (2 * TREE_MAXLV + 1), c->stream));
+    HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * (2 * TREE_MAXLV + 2), c->stream));
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
     u64 gbase = 0, cbase = 0, pgbase = 0, pcbase = 0;
     for (int l = 0; l <= L.N; ++l) {
@@ -1965,7 +1970,8 @@ int run_tree(tlcg_ctx* c) {
       a.lvl = ctr;
       a.lvl_gen = ctr + TREE_MAXLV;
       a.flags = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV);
-      if (!launch_tree(a, cap, c->stream)) {
+      a.max_n = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV + 1);
+      if (!launch_tree(a, cap, groups, c->stream)) {
         c->err = "component-tree kernel launch failed";
         return -1;
       }
@@ -1975,7 +1981,7 @@ int run_tree(tlcg_ctx* c) {
       cbase += a.n_comp;
     }
     HIPCHK_I(hipEventRecord(c->e1, c->stream));
-    HIPCHK_I(hipMemcpyAsync(c->h_tree_ctr, ctr, sizeof(unsigned long long) * (2 * TREE_MAXLV + 1),
+    HIPCHK_I(hipMemcpyAsync(c->h_tree_ctr, ctr, sizeof(unsigned long long) * (2 * TREE_MAXLV + 2),
                             hipMemcpyDeviceToHost, c->stream));
     HIPCHK_I(hipStreamSynchronize(c->stream));
     float ms = 0;
@@ -1986,6 +1992,23 @@ int run_tree(tlcg_ctx* c) {
     if (flags & TREE_EVENT) return 0;  // the global engine finds TLC's first error and its trace
     if (flags & TREE_OVERFLOW) continue;
     c->tree_cap = cap;
+    if (std::getenv("TLCG_TREE_STATS")) {  // diagnostics: component sizes per layer
+      std::vector<uint32_t> nn(comps);
+      HIPCHK_I(hipMemcpy(nn.data(), c->d_tree_n, comps * 4, hipMemcpyDeviceToHost));
+      u64 b0 = 0;
+      for (size_t l = 0; l < ncomp.size(); ++l) {
+        uint32_t mx = 0, mn = ~0u;
+        double sum = 0;
+        for (u64 i = 0; i < ncomp[l]; ++i) {
+          mx = std::max(mx, nn[b0 + i]);
+          mn = std::min(mn, nn[b0 + i]);
+          sum += nn[b0 + i];
+        }
+        std::fprintf(stderr, "tree layer %zu: %llu components, states min %u avg %.1f max %u\n", l,
+                     (unsigned long long)ncomp[l], mn, sum / (double)ncomp[l], mx);
+        b0 += ncomp[l];
+      }
+    }
     c->passes.clear();
     c->comp_levels.assign(c->h_tree_ctr, c->h_tree_ctr + TREE_MAXLV);
     c->comp_level_gen.assign(c->h_tree_ctr + TREE_MAXLV, c->h_tree_ctr + 2 * TREE_MAXLV);
