@@ -110,3 +110,51 @@ def test_p8_on_the_tree():
         assert (r2.generated, r2.distinct, r2.levels) == (r.generated, r.distinct, r.levels)
     finally:
         ck.close()
+
+
+INVARIANTS = ["TypeSafe", "CompactedLedgerLeak", "CompactionHorizonCorrectness", "DuplicateNullKeyMessage"]
+
+
+def random_producer_model(seed):
+    """A seeded producer-modelled constant set (every other knob drawn too),
+    small enough for the C oracle to finish in well under a second."""
+    rng = random.Random(1000 + seed)
+    return tlcgpu.Model(msg_sent_limit=rng.randint(1, 3), compaction_times_limit=rng.choice([1, 2, 3, 4]),
+                        max_crash_times=rng.randint(0, 2), consume_times_limit=rng.randint(0, 2),
+                        model_consumer=rng.random() < 0.3, model_producer=True,
+                        retain_null_key=rng.random() < 0.6,
+                        key_space=sorted(rng.sample(range(1, 9), rng.randint(0, 2))),
+                        value_space=sorted(rng.sample(range(1, 9), rng.randint(0, 2))),
+                        invariants=rng.sample(INVARIANTS, rng.randint(1, 4)), check_deadlock=rng.random() < 0.5)
+
+
+def tree_applies(m):
+    """the tree keeps 31-bit local keys: the state above `messages` and its
+    length (csrc/model.h layout; tree_applicable in csrc/tlcgpu.hip)"""
+    n = m.msg_sent_limit
+    kb = len(m.key_space).bit_length()    # key indices 0..|KeySpace| (0 = NullKey)
+    vb = len(m.value_space).bit_length()
+    mb = n.bit_length() + n * (kb + vb)
+    return tlcgpu.state_words(m) == 1 and tlcgpu.state_bits(m) - mb <= 31
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_tree_random_producer_cfgs(seed):
+    """Seeded random producer-modelled cfgs against the C oracle run live: the
+    tree's counts and every level when the check passes, and on an error the
+    global engine's verdict and depth (the tree hands the model over)."""
+    from conftest import run_oracle
+    m = random_producer_model(seed)
+    if tlcgpu.check_model(m) is not None:
+        pytest.skip(f"constants refused: {tlcgpu.check_model(m)}")
+    want = run_oracle(m)
+    r = tlcgpu.run(m)
+    assert r.status == want["result"], (seed, r.status, want["result"])
+    assert r.depth == want["depth"], seed
+    if want["result"] == "ok":
+        assert (r.generated, r.distinct, r.levels) == (want["generated"], want["distinct"], want["levels"]), seed
+        assert r.engine == ("tree" if tree_applies(m) else "global"), (seed, r.engine)
+    else:
+        assert r.engine == "global", seed
+        if want["result"] in ("invariant", "invariant_error"):
+            assert r.invariant == want["invariant"], seed
