@@ -402,7 +402,8 @@ def main():
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
         return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                    kernel="k_tree<512> (component tree, one wavefront per messages value)",
+                    kernel=("tlcg_tree_384 (hipRTC-specialized" if r["jit"] & 1 else "k_tree<384, 512, 4> (") +
+                    "component tree, 4 components per wavefront)",
                     launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
                     bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, kernel_bytes_per_distinct=TREE_BYTES_PER_STATE,
                     kernel_written_gbs=round(TREE_BYTES_PER_STATE * distinct / world / (r["expand_ms"] * 1e-3) / 1e9,

@@ -62,6 +62,10 @@ std::string program_source(const Layout& L) {
              "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ", " + od + ", " + code +
              ">(a, kL); }\n";
       }
+  s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_384(tlcg::TreeArgs a) "
+       "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";
+  s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_1024(tlcg::TreeArgs a) "
+       "{ tlcg::tree_body<1024, 2048, 1>(a, kL); }\n";
   return s;
 }
 
@@ -159,6 +163,13 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
         *err = "hipModuleGetFunction " + n;
         return false;
       }
+      if (i < 2 && od == 0) {
+        const char* tn = i == 0 ? "tlcg_tree_384" : "tlcg_tree_1024";
+        if (hipModuleGetFunction(&out->tree[i], out->module, tn) != hipSuccess) {
+          *err = std::string("hipModuleGetFunction ") + tn;
+          return false;
+        }
+      }
       if (i < 2) {
         const std::string nc = std::string(od ? "tlcg_componentcod_" : "tlcg_componentc_") + names[i];
         if (hipModuleGetFunction(od ? &out->code_od[i] : &out->code[i], out->module, nc.c_str()) != hipSuccess) {
@@ -185,6 +196,16 @@ bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool co
   CompArgs copy = a;
   void* args[] = {&copy};
   return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
+}
+
+bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream) {
+  if (!a.n_comp) return true;
+  hipFunction_t f = cap == 384 ? k.tree[0] : k.tree[1];
+  if (!f) return false;
+  TreeArgs copy = a;
+  void* args[] = {&copy};
+  return hipModuleLaunchKernel(f, tree_grid(a.n_comp, cap == 384 ? 4 : 1), 1, 1, 64, 1, 1, 0, stream, args, nullptr) ==
+         hipSuccess;
 }
 
 }  // namespace tlcg

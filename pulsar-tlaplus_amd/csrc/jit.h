@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "component.h"
+#include "tree.h"
 
 namespace tlcg {
 
@@ -17,6 +18,7 @@ struct JitKernels {
   hipFunction_t component_od[4] = {nullptr, nullptr, nullptr, nullptr};  // the same, counting outdegrees
   hipFunction_t code[2] = {nullptr, nullptr};     // component codes (component_code.h), K = 32, 64
   hipFunction_t code_od[2] = {nullptr, nullptr};
+  hipFunction_t tree[2] = {nullptr, nullptr};     // component tree: 384 slots x 4 groups, 1024 slots x 1
   double compile_s = 0;  // 0 when loaded from the cache
   bool cached = false;
 };
@@ -28,5 +30,7 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err);
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err);
 void jit_release(JitKernels* k);
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream);
+// the specialized tree kernel for cap 384 (4 groups) or 1024 (1 group); false when not built or on a launch error
+bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream);
 
 }  // namespace tlcg

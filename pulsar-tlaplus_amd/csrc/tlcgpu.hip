@@ -1923,6 +1923,16 @@ int run_tree(tlcg_ctx* c) {
   // components per wavefront (tuning hook TLCG_TREE_G = 1 / 2 / 4)
   int groups = 4;
   if (const char* gv = std::getenv("TLCG_TREE_G")) groups = std::atoi(gv) == 1 ? 1 : std::atoi(gv) == 2 ? 2 : 4;
+  // the layout-specialized kernels (jit.cpp) when the tree is large enough
+  // to repay a hipRTC compile (env TLCG_JIT=0/1 forces)
+  const char* jv = std::getenv("TLCG_JIT");
+  const bool want_jit = (jv ? std::atoi(jv) != 0 : comps >= 4096) && groups == 4;
+  if (want_jit && c->jit_state == 0) {
+    std::string e;
+    c->jit_state = jit_build(L, c->opts.device, &c->jit, &e) ? 1 : -1;
+    if (c->jit_state < 0) c->jit_error = e;
+  }
+  c->jit_used = want_jit && c->jit_state == 1;
   for (int cap : {384, 1024}) {
     const u64 slots = comps * (u64)cap;
     // the store (state + parent), the depth bytes and the sizes must fit next to what is allocated
@@ -1971,7 +1981,8 @@ int run_tree(tlcg_ctx* c) {
       a.lvl_gen = ctr + TREE_MAXLV;
       a.flags = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV);
       a.max_n = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV + 1);
-      if (!launch_tree(a, cap, groups, c->stream)) {
+      if (!(c->jit_used && (cap == 384 || cap == 1024) ? jit_launch_tree(c->jit, a, cap, c->stream)
+                                                        : launch_tree(a, cap, cap == 384 ? groups : 1, c->stream))) {
         c->err = "component-tree kernel launch failed";
         return -1;
       }

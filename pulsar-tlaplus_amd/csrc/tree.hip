@@ -1,202 +1,22 @@
-// pulsar-tlaplus_amd/csrc/tree.hip -- the component-tree engine's kernel
-// (tree.h): a wavefront runs G components of a layer at once, one per group
-// of 64 / G lanes, each with its FPSet in LDS; a component's BFS is a
-// multi-source BFS whose sources are its parent component's states with the
-// component's message appended.
+// pulsar-tlaplus_amd/csrc/tree.hip -- precompiled component-tree kernels
+// (runtime layout); jit.cpp builds layout-specialized ones from the same
+// tree_body.h.
 #include "tree.h"
 
-#include "component_model.h"
-#include "kernels.h"
+#include "tree_body.h"
 
 namespace tlcg {
 
 namespace {
 
-// CAP states per component, T FPSet slots (a power of 2, load <= CAP / T),
-// G components per wavefront.  A component's depth holds ~16 states, so one
-// component per 64-lane wavefront leaves most lanes idle and pays the
-// scalar (exec-mask, loop) instructions once per state; G groups share them.
 template <int CAP, int T, int G>
 __global__ __launch_bounds__(64) void k_tree(TreeArgs a) {
-  constexpr int S = 64 / G;  // lanes per group
-  static_assert((T & (T - 1)) == 0 && T >= CAP, "T: a power of 2 >= CAP");
-  __shared__ uint32_t h[G][T];       // local key + 1, 0 = empty
-  __shared__ uint32_t keys[G][CAP];  // each component's local keys in BFS (depth) order
-  __shared__ unsigned long long lvl_d[TREE_MAXLV], lvl_g[TREE_MAXLV];
-  const Layout& L = a.L;
-  const int lane = threadIdx.x;
-  const int g = lane / S, sub = lane % S;
-  const u64 gmask = (S == 64 ? ~0ull : ((1ull << S) - 1)) << (g * S);  // my group's lanes
-  const u64 below = lanemask_lt() & gmask;
-  const int mb = L.msg_sh + L.N * L.mw;  // `messages` (with its length) occupies the low mb bits
-  int log2t = 0;
-  while ((1 << log2t) < T) ++log2t;
-  for (int i = lane; i < TREE_MAXLV; i += 64) lvl_d[i] = lvl_g[i] = 0;
-  __syncthreads();
-  unsigned flags = 0;
-  uint32_t maxn = 0;
-  // a group's current component and its BFS state (uniform inside the group)
-  u64 ci = (u64)blockIdx.x * G + (u64)g;
-  const u64 cstep = (u64)gridDim.x * G;
-  bool have = false;
-  u64 np = 0, pc = 0, e = 0, msgs = 0;
-  int j = 0, nprod = 0, n = 0, f0 = 0, d = 0;
-  CompMsgs cm{};
-  const u64* pst = nullptr;
-  const uint8_t* pdep = nullptr;
-  u64 pgb = 0, gb = 0;
-  u64 *st = nullptr, *par = nullptr;
-  uint8_t* dp = nullptr;
-  uint32_t* hh = &h[g][0];
-  uint32_t* kk = &keys[g][0];
-  // insert the group's candidates (pred) at depth dd: LDS CAS on the key, the
-  // new ones appended in lane order
-  auto insert = [&](bool pred, lkey key, u64 pref, int dd) {
-    bool isnew = false;
-    if (pred) {
-      unsigned s = (key * 0x9E3779B1u) >> (32 - log2t);
-      for (int p = 0; p < T; ++p) {
-        const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
-        if (old == 0) {
-          isnew = true;
-          break;
-        }
-        if (old == key + 1u) break;
-        s = (s + 1) & (T - 1);
-      }
-    }
-    const u64 m = __ballot(isnew) & gmask;
-    const int cnt = __popcll(m);
-    if (n + cnt > CAP) {
-      if (have) flags |= TREE_OVERFLOW;
-    } else if (isnew) {
-      const int pos = n + __popcll(m & below);
-      kk[pos] = key;
-      st[pos] = msgs | ((u64)key << mb);
-      par[pos] = pref == NO_PARENT ? NO_PARENT : (a.rank_tag | pref);
-      dp[pos] = (uint8_t)dd;
-      if (check_invariants_k(L, cm, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
-    }
-    n = n + cnt > CAP ? CAP : n + cnt;
-  };
-  while (true) {
-    // a group without a component takes its next one
-    if (!have && ci < a.n_comp) {
-      for (int i = sub * 4; i < T; i += S * 4) *reinterpret_cast<uint4*>(&hh[i]) = make_uint4(0, 0, 0, 0);
-      if (a.layer == 0) {
-        np = a.n_init;
-        pc = 0;
-        j = 0;
-      } else {
-        pc = ci / (u64)L.nkv;
-        j = (int)(ci % (u64)L.nkv);
-        np = a.par_n[pc];
-      }
-      pst = a.layer ? a.par_states + pc * CAP : nullptr;
-      pdep = a.layer ? a.par_dep + pc * CAP : nullptr;
-      pgb = a.par_gbase + pc * CAP;
-      const u64 w0 = a.layer == 0 ? init_state(L, 0) : producer_succ(L, pst[0], a.layer - 1, j);
-      msgs = w0 & L.msgs_mask;
-      cm = comp_msgs_init(L, w0);  // everything that reads only `messages`
-      nprod = cm.len < L.N ? L.nkv : 0;  // Producer's successors (into the children)
-      st = a.states + ci * CAP;
-      par = a.parents + ci * CAP;
-      dp = a.dep + ci * CAP;
-      gb = a.gbase + ci * CAP;
-      n = f0 = d = 0;
-      e = 0;
-      have = true;
-    }
-    if (!__ballot(have)) break;
-    __syncthreads();
-    // the next depth: the frontier's, or past a gap the next entries'; a
-    // component with neither is complete
-    if (have && f0 == n) {
-      if (e >= np) {  // (the group sits out the rest of this pass)
-        if (sub == 0) a.n_out[ci] = (uint32_t)n;
-        maxn = n > (int)maxn ? (uint32_t)n : maxn;
-        have = false;
-        ci += cstep;
-      } else {
-        d = a.layer == 0 ? 0 : (int)pdep[e] + 1;
-      }
-    }
-    if (have && d >= TREE_MAXLV - 1) flags |= TREE_OVERFLOW;
-    // the entries at depth d (parents at depth d - 1; pdep is nondecreasing)
-    bool more = have && e < np;
-    while (__ballot(more)) {
-      const u64 i = e + (u64)sub;
-      bool ok = more && i < np;
-      lkey key = 0;
-      u64 pref = NO_PARENT;
-      if (ok && a.layer == 0) {
-        key = (lkey)(init_state(L, i) >> mb);
-      } else if (ok) {
-        ok = (int)pdep[i] + 1 == d;
-        key = (lkey)(producer_succ(L, pst[i], a.layer - 1, j) >> mb);
-        pref = ((pgb + i) << L.ord_bits) | (u64)ordinal_of(L, ACT_PRODUCER, j);
-      }
-      insert(ok, key, pref, d);
-      const int taken = __popcll(__ballot(ok) & gmask);
-      e += (u64)taken;
-      more = more && taken == S && e < np;
-    }
-    __syncthreads();
-    const int f1 = n;  // depth d = [f0, f1)
-    // expand depth d: compactor and BrokerCrash successors at depth d + 1
-    u64 gen = 0;
-    for (int b = f0; __ballot(have && b < f1); b += S) {
-      const int i = b + sub;
-      const bool ok = have && i < f1;
-      const lkey k = ok ? kk[i] : 0;
-      lkey t = 0, t2 = 0;
-      int act = 0;
-      const int r = ok ? compactor_step_k(L, cm, msgs, k, k_phase(L, k), &t, &act) : 0;
-      const bool crash = ok && crash_step_k(L, k, &t2);
-      const int nsucc = nprod + (r == 1) + (int)crash + selfloop_count_k(L, cm, k);
-      if (ok) {
-        gen += (u64)nsucc;
-        if (r == 2 || (nsucc == 0 && L.check_deadlock)) flags |= TREE_EVENT;
-      }
-      const u64 pref = (gb + (u64)i) << L.ord_bits;
-      insert(r == 1, t, pref | (u64)ordinal_of(L, act, 0), d + 1);
-      insert(crash, t2, pref | (u64)ordinal_of(L, ACT_CRASH, 0), d + 1);
-    }
-    // the group's sum of generated successors, added by its first lane
-#pragma unroll
-    for (int off = S / 2; off > 0; off >>= 1) gen += __shfl_xor(gen, off);
-    if (have && sub == 0 && d < TREE_MAXLV) {
-      atomicAdd(&lvl_d[d], (unsigned long long)(f1 - f0));
-      atomicAdd(&lvl_g[d], gen);
-    }
-    __syncthreads();
-    if (have) {
-      f0 = f1;
-      ++d;
-    }
-    if (__ballot(flags != 0)) break;  // the global engine takes the model
-  }
-  // fold the lanes' flags and the largest component, then the per-depth counts
-  const unsigned fl = __ballot(flags & TREE_EVENT) ? TREE_EVENT : 0;
-  const unsigned fo = __ballot(flags & TREE_OVERFLOW) ? TREE_OVERFLOW : 0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) maxn = max(maxn, (uint32_t)__shfl_xor(maxn, off));
-  if (lane == 0) {
-    if (fl | fo) atomicOr(a.flags, fl | fo);
-    atomicMax(a.max_n, maxn);
-  }
-  __syncthreads();
-  for (int i = lane; i < TREE_MAXLV; i += 64) {
-    if (lvl_d[i]) atomicAdd(&a.lvl[i], lvl_d[i]);
-    if (lvl_g[i]) atomicAdd(&a.lvl_gen[i], lvl_g[i]);
-  }
+  tree_body<CAP, T, G>(a, a.L);
 }
 
 template <int CAP, int T, int G>
 void launch_g(const TreeArgs& a, hipStream_t stream) {
-  const u64 wgs = (a.n_comp + G - 1) / G;
-  const unsigned grid = (unsigned)(wgs < 16384 ? wgs : 16384);
-  k_tree<CAP, T, G><<<grid, 64, 0, stream>>>(a);
+  k_tree<CAP, T, G><<<tree_grid(a.n_comp, G), 64, 0, stream>>>(a);
 }
 
 }  // namespace
