@@ -42,7 +42,6 @@ BYTES_PER_STATE_WORD = 8
 PMC_PROFILE = "pmc_k_expand.json"
 PMC_COMPONENT_PROFILE = "pmc_component.json"
 COMPONENT_BYTES_PER_STATE = 16  # state word + parent entry written to the HBM store
-TREE_BYTES_PER_STATE = 17       # the same + the state's depth byte (read back by the next layer)
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
 # algorithmic HBM bytes per distinct state of the BFS path (read
 # the frontier state 8 B, write the new state 8 B and its parent entry 8 B,
@@ -238,7 +237,8 @@ def main():
         counts = [st.generated, st.distinct]
         used = tlcgpu.ENGINE_NAMES.get(int(st.engine), "?")
         jit = int(st.jit_used)
-        launches = len(eng.level_sizes()) if used == "global" else cfg.get("N", 3) + 1 if used == "tree" else 1
+        launches = len(eng.level_sizes()) if used == "global" else \
+            cfg.get("N", 3) + 1 if used == "tree" and cfg.get("producer") else 1
         if distributed:
             t = torch.tensor([elapsed, ems, kms], dtype=torch.float64, device=rdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -396,18 +396,23 @@ def main():
 
     def roofline_tree(r):
         # SURVEY 8(d)'s per-unit figure x the distinct states of one step; the
-        # kernel writes 17 B/state (state, parent entry, depth byte) and reads
-        # 9 B per entry (its parent state and depth); its FPSets stay in LDS
+        # kernel writes the state word(s) and the parent entry per state (and,
+        # Producer modelled, a depth byte the next layer reads with the parent
+        # state, 9 B per entry); its FPSets stay in LDS
         bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
+        per_state = BYTES_PER_STATE_WORD * (words + 1) + (1 if open_model else 0)
+        if open_model:
+            kern = ("tlcg_tree_384 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<384, 512, 4> (") + \
+                "component tree, 4 components per wavefront)"
+        else:
+            kern = ("tlcg_treec_640 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<640, 1024, 4, closed> (") + \
+                "component tree closed mode: component codes, 4 components per wavefront)"
         return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                    kernel=("tlcg_tree_384 (hipRTC-specialized" if r["jit"] & 1 else "k_tree<384, 512, 4> (") +
-                    "component tree, 4 components per wavefront)",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kern,
                     launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                    bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, kernel_bytes_per_distinct=TREE_BYTES_PER_STATE,
-                    kernel_written_gbs=round(TREE_BYTES_PER_STATE * distinct / world / (r["expand_ms"] * 1e-3) / 1e9,
-                                             1))
+                    bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, kernel_bytes_per_distinct=per_state,
+                    kernel_written_gbs=round(per_state * distinct / world / (r["expand_ms"] * 1e-3) / 1e9, 1))
 
     def summary(r):
         out = dict(engine=r["engine"], jit=bool(r["jit"]), value=round(distinct * args.steps / r["elapsed"], 1),

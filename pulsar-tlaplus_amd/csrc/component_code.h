@@ -125,6 +125,39 @@ TLCG_HD lkey code_decode(const Layout& L, const CodeConsts& K, ckey c) {
   return k;
 }
 
+// the same for a whole state word of either width (wide layouts, whose
+// local keys exceed 32 bits: the component tree's closed mode)
+template <typename W>
+TLCG_HD ckey code_encode_w(const Layout& L, W s) {
+  ckey c = 0;
+  for (int j = 1; j <= L.C; ++j) c |= (ckey)led_present<W>(L, s, j) << (j - 1);
+  c |= (ckey)(st_p1r<W>(L, s) != 0) << cc_r(L);
+  c |= (ckey)(st_hz<W>(L, s) != 0) << cc_h(L);
+  c |= (ckey)st_phase<W>(L, s) << cc_ph(L);
+  c |= (ckey)st_ctx<W>(L, s) << cc_x(L);
+  c |= (ckey)cur_present<W>(L, s) << cc_cp(L);
+  c |= (ckey)(cur_h<W>(L, s) != 0) << cc_ch(L);
+  c |= (ckey)cur_c<W>(L, s) << cc_cc(L);
+  c |= (ckey)st_crash<W>(L, s) << cc_cr(L);
+  return c;
+}
+// code -> the state word msgs | (its local fields); ledbits as in CodeConsts
+template <typename W>
+TLCG_HD W code_word(const Layout& L, const CodeConsts& K, W msgs, ckey c) {
+  W s = msgs;
+  for (int j = 1; j <= L.C; ++j)
+    if ((c >> (j - 1)) & 1) s = fset<W>(s, led_base(L, j), L.led_w, (u64)K.ledbits);
+  if ((c >> cc_r(L)) & 1) s = fset<W>(s, L.p1r_sh, L.p1r_w, K.len);
+  s = fset<W>(s, L.ph_sh, 3, cget(c, cc_ph(L), 3));
+  if ((c >> cc_h(L)) & 1) s = fset<W>(s, L.hz_sh, L.hz_w, K.len);
+  s = fset<W>(s, L.ctx_sh, L.ctx_w, cget(c, cc_x(L), L.ctx_w));
+  if ((c >> cc_cp(L)) & 1) {
+    const u64 h = ((c >> cc_ch(L)) & 1) ? K.len : 0u;
+    s = fset<W>(s, L.cur_sh, 1 + L.curh_w + L.curc_w, 1ull | (h << 1) | ((u64)cget(c, cc_cc(L), L.curc_w) << (1 + L.curh_w)));
+  }
+  return fset<W>(s, L.cr_sh, L.cr_w, cget(c, cc_cr(L), L.cr_w));
+}
+
 TLCG_HD int c_phase(const Layout& L, ckey c) { return (int)cget(c, cc_ph(L), 3); }
 // MaxCompactedLedgerId, compaction.tla:103-106
 TLCG_HD int c_max_ledger(const Layout& L, ckey c) {

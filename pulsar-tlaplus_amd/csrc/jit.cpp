@@ -66,6 +66,15 @@ std::string program_source(const Layout& L) {
        "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_1024(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<1024, 2048, 1>(a, kL); }\n";
+  // the closed mode on this layout's word (u64, or u128 past 63 bits)
+  const std::string w = L.bits <= 63 ? "tlcg::u64" : "tlcg::u128";
+  // (TLCG_TREEC_G: components per wavefront of the closed mode, a tuning
+  // hook; the launch grid is the same, the kernel strides over the rest)
+  s += "#ifndef TLCG_TREEC_G\n#define TLCG_TREEC_G 4\n#endif\n";
+  s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treec_640(tlcg::TreeArgs a) "
+       "{ tlcg::tree_body<640, 1024, TLCG_TREEC_G, true, " + w + ">(a, kL); }\n";
+  s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treec_2048(tlcg::TreeArgs a) "
+       "{ tlcg::tree_body<2048, 4096, 1, true, " + w + ">(a, kL); }\n";
   return s;
 }
 
@@ -163,8 +172,8 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
         *err = "hipModuleGetFunction " + n;
         return false;
       }
-      if (i < 2 && od == 0) {
-        const char* tn = i == 0 ? "tlcg_tree_384" : "tlcg_tree_1024";
+      if (od == 0) {
+        const char* tn = i == 0 ? "tlcg_tree_384" : i == 1 ? "tlcg_tree_1024" : i == 2 ? "tlcg_treec_640" : "tlcg_treec_2048";
         if (hipModuleGetFunction(&out->tree[i], out->module, tn) != hipSuccess) {
           *err = std::string("hipModuleGetFunction ") + tn;
           return false;
@@ -200,12 +209,12 @@ bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool co
 
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream) {
   if (!a.n_comp) return true;
-  hipFunction_t f = cap == 384 ? k.tree[0] : k.tree[1];
+  hipFunction_t f = cap == 384 ? k.tree[0] : cap == 1024 ? k.tree[1] : cap == 640 ? k.tree[2] : k.tree[3];
   if (!f) return false;
   TreeArgs copy = a;
   void* args[] = {&copy};
-  return hipModuleLaunchKernel(f, tree_grid(a.n_comp, cap == 384 ? 4 : 1), 1, 1, 64, 1, 1, 0, stream, args, nullptr) ==
-         hipSuccess;
+  const int groups = cap == 384 || cap == 640 ? 4 : 1;
+  return hipModuleLaunchKernel(f, tree_grid(a.n_comp, groups), 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
 }
 
 }  // namespace tlcg

@@ -18,7 +18,8 @@ struct JitKernels {
   hipFunction_t component_od[4] = {nullptr, nullptr, nullptr, nullptr};  // the same, counting outdegrees
   hipFunction_t code[2] = {nullptr, nullptr};     // component codes (component_code.h), K = 32, 64
   hipFunction_t code_od[2] = {nullptr, nullptr};
-  hipFunction_t tree[2] = {nullptr, nullptr};     // component tree: 384 slots x 4 groups, 1024 slots x 1
+  hipFunction_t tree[4] = {nullptr, nullptr, nullptr, nullptr};  // component tree: 384 x 4 groups, 1024 x 1;
+                                                                 // closed mode: 640 x 4, 2048 x 1
   double compile_s = 0;  // 0 when loaded from the cache
   bool cached = false;
 };
@@ -30,7 +31,8 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err);
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err);
 void jit_release(JitKernels* k);
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream);
-// the specialized tree kernel for cap 384 (4 groups) or 1024 (1 group); false when not built or on a launch error
+// the specialized tree kernel for cap 384 / 640 (4 groups) or 1024 / 2048 (1 group); false when not built or on a
+// launch error
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream);
 
 }  // namespace tlcg

@@ -1901,17 +1901,39 @@ bool tree_applicable(const tlcg_ctx* c) {
          !c->opts.device_store_cap && !c->opts.fpset_spill;
 }
 
-// Run every layer of the component tree: chunks of 384 states per component
-// (the shipped N = 3, C = 3, K = 1 have at most 359), then 1024 if one
-// overflows.  Returns 1 done, 0 the global engine takes the model (an event
-// to report as TLC does, a component past 1024 states or TREE_MAXLV depths,
-// or not enough memory), -1 error.
+// the closed mode (tree.h): no Producer, a closed partition, components the
+// component engine could not take (local keys over 32 bits, or more than 255
+// states), codes of <= 31 bits (the LDS table stores code + 1)
+bool tree_closed_applicable(const tlcg_ctx* c) {
+  const Layout& L = c->hm.L;
+  const char* tv = std::getenv("TLCG_TREE");
+  return !L.producer && !(tv && std::atoi(tv) == 0) && c->closed && !c->opts.tlc_order && !c->opts.outdegree &&
+         code_bits(L) <= 31 && L.N >= 1 && L.N <= 8 && (c->words == 1 || c->words == 2) &&
+         c->hm.n_init >= 1 && c->hm.n_init < (1ull << 40) && !c->opts.device_store_cap && !c->opts.fpset_spill;
+}
+
+// Run the component tree.  Producer modelled: every layer, chunks of 384
+// states per component (the shipped N = 3, C = 3, K = 1 have at most 359),
+// then 1024 if one overflows.  Closed: this rank's components (a contiguous
+// range of initial states) in one launch, chunks of 640 states (557 at
+// CompactionTimesLimit = 12), then 2048.  Returns 1 done, 0 the global engine
+// takes the model (an event to report as TLC does, a component past the
+// capacity or TREE_MAXLV depths, or not enough memory), -1 error.
 int run_tree(tlcg_ctx* c) {
   const Layout& L = c->hm.L;
-  std::vector<u64> ncomp(1, 1);  // components per layer: nkv^l
-  for (int l = 1; l <= L.N; ++l) {
-    if (ncomp.back() > (1ull << 34) / (u64)L.nkv) return 0;
-    ncomp.push_back(ncomp.back() * (u64)L.nkv);
+  const bool closed = !L.producer;
+  std::vector<u64> ncomp;  // components per launch (layer): nkv^l, or this rank's initial states
+  u64 r0 = 0;
+  if (closed) {
+    const u64 W = (u64)c->opts.world, R = (u64)c->opts.rank;
+    r0 = c->hm.n_init * R / W;
+    ncomp.push_back(c->hm.n_init * (R + 1) / W - r0);
+  } else {
+    ncomp.push_back(1);
+    for (int l = 1; l <= L.N; ++l) {
+      if (ncomp.back() > (1ull << 34) / (u64)L.nkv) return 0;
+      ncomp.push_back(ncomp.back() * (u64)L.nkv);
+    }
   }
   u64 comps = 0;
   for (u64 x : ncomp) comps += x;
@@ -1923,6 +1945,7 @@ int run_tree(tlcg_ctx* c) {
   // components per wavefront (tuning hook TLCG_TREE_G = 1 / 2 / 4)
   int groups = 4;
   if (const char* gv = std::getenv("TLCG_TREE_G")) groups = std::atoi(gv) == 1 ? 1 : std::atoi(gv) == 2 ? 2 : 4;
+  if (closed && groups == 1) groups = 2;
   // the layout-specialized kernels (jit.cpp) when the tree is large enough
   // to repay a hipRTC compile (env TLCG_JIT=0/1 forces)
   const char* jv = std::getenv("TLCG_JIT");
@@ -1933,17 +1956,19 @@ int run_tree(tlcg_ctx* c) {
     if (c->jit_state < 0) c->jit_error = e;
   }
   c->jit_used = want_jit && c->jit_state == 1;
-  for (int cap : {384, 1024}) {
+  const int words = c->words;
+  for (int cap : closed ? std::vector<int>{640, 2048} : std::vector<int>{384, 1024}) {
     const u64 slots = comps * (u64)cap;
-    // the store (state + parent), the depth bytes and the sizes must fit next to what is allocated
+    // the store (state words + parent), the depth bytes and the sizes must fit next to what is allocated
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
-    const double have = (double)fr + 16.0 * (double)c->cap + (double)c->tree_slots + 4.0 * (double)c->tree_comps;
-    if (17.0 * (double)slots + 4.0 * (double)comps > 0.85 * have) return 0;
+    const double per_slot = 8.0 * (words + 1) + (closed ? 0.0 : 1.0);
+    const double have = (double)fr + 8.0 * (words + 1) * (double)c->cap + (double)c->tree_slots + 4.0 * (double)c->tree_comps;
+    if (per_slot * (double)slots + 4.0 * (double)comps > 0.85 * have) return 0;
     c->engine = TLCG_ENGINE_TREE;
     c->comp_store_used = 0;  // nothing of an earlier run to keep (tlcg_init freed the host chunks)
     if (!ensure_store(c, slots)) return -1;
-    if (c->tree_slots < slots) {
+    if (!closed && c->tree_slots < slots) {
       hipFree(c->d_tree_dep);
       c->d_tree_dep = nullptr;
       c->tree_slots = 0;
@@ -1961,19 +1986,20 @@ int run_tree(tlcg_ctx* c) {
     HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * (2 * TREE_MAXLV + 2), c->stream));
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
     u64 gbase = 0, cbase = 0, pgbase = 0, pcbase = 0;
-    for (int l = 0; l <= L.N; ++l) {
+    for (size_t l = 0; l < ncomp.size(); ++l) {
       TreeArgs a;
       a.L = L;
-      a.layer = l;
-      a.n_comp = ncomp[(size_t)l];
+      a.layer = (int)l;
+      a.n_comp = ncomp[l];
       a.n_init = c->hm.n_init;
+      a.comp0 = r0;
       a.par_states = l ? c->d_states + pgbase : nullptr;
       a.par_dep = l ? c->d_tree_dep + pgbase : nullptr;
       a.par_n = l ? c->d_tree_n + pcbase : nullptr;
       a.par_gbase = pgbase;
-      a.states = c->d_states + gbase;
+      a.states = c->d_states + gbase * (u64)words;
       a.parents = c->d_parents + gbase;
-      a.dep = c->d_tree_dep + gbase;
+      a.dep = closed ? nullptr : c->d_tree_dep + gbase;
       a.n_out = c->d_tree_n + cbase;
       a.gbase = gbase;
       a.rank_tag = (u64)c->opts.rank << 56;
@@ -1981,8 +2007,9 @@ int run_tree(tlcg_ctx* c) {
       a.lvl_gen = ctr + TREE_MAXLV;
       a.flags = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV);
       a.max_n = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV + 1);
-      if (!(c->jit_used && (cap == 384 || cap == 1024) ? jit_launch_tree(c->jit, a, cap, c->stream)
-                                                        : launch_tree(a, cap, cap == 384 ? groups : 1, c->stream))) {
+      const bool jit = c->jit_used && (cap == 384 || cap == 1024 || cap == 640 || cap == 2048);
+      const int g = cap == 384 || cap == 640 ? groups : 1;
+      if (!(jit ? jit_launch_tree(c->jit, a, cap, c->stream) : launch_tree(a, cap, g, closed, words, c->stream))) {
         c->err = "component-tree kernel launch failed";
         return -1;
       }
@@ -2024,7 +2051,7 @@ int run_tree(tlcg_ctx* c) {
     c->comp_levels.assign(c->h_tree_ctr, c->h_tree_ctr + TREE_MAXLV);
     c->comp_level_gen.assign(c->h_tree_ctr + TREE_MAXLV, c->h_tree_ctr + 2 * TREE_MAXLV);
     while (!c->comp_levels.empty() && c->comp_levels.back() == 0) c->comp_levels.pop_back();
-    c->comp_init = c->hm.n_init;
+    c->comp_init = closed ? ncomp[0] : c->hm.n_init;
     c->comp_distinct = 0;
     for (u64 x : c->comp_levels) c->comp_distinct += x;
     c->comp_generated = c->comp_init;
@@ -2035,7 +2062,7 @@ int run_tree(tlcg_ctx* c) {
     c->status = TLCG_DONE;
     return 1;
   }
-  return 0;  // a component past 1024 states
+  return 0;  // a component past the largest chunk
 }
 
 bool run_init(tlcg_ctx* c) {
@@ -2349,7 +2376,7 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
     *out = c;
     return -2;
   }
-  if (c->opts.engine == TLCG_ENGINE_TREE && !tree_applicable(c)) {
+  if (c->opts.engine == TLCG_ENGINE_TREE && !tree_applicable(c) && !tree_closed_applicable(c)) {
     c->err = "the component-tree engine needs a modelled Producer, one rank, <= 63-bit states, no TLC-order "
              "mode and no outdegree statistics";
     *out = c;
@@ -2460,7 +2487,7 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
       return 0;
     }
   }
-  if (c->opts.engine != TLCG_ENGINE_GLOBAL && component_applicable(c)) {
+  if (c->opts.engine != TLCG_ENGINE_GLOBAL && c->opts.engine != TLCG_ENGINE_TREE && component_applicable(c)) {
     // the component engine runs the whole BFS here; 0 = a component needs the global engine
     const int r = run_component(c);
     if (r < 0) return -10;
@@ -2472,6 +2499,16 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
     if (c->opts.engine == TLCG_ENGINE_COMPONENT) {
       c->err = "a component does not fit on chip (over 255 states or 48 levels); use the global engine";
       return -12;
+    }
+  }
+  if ((c->opts.engine == TLCG_ENGINE_AUTO || c->opts.engine == TLCG_ENGINE_TREE) && tree_closed_applicable(c)) {
+    // components too large for a lane: the component tree's closed mode
+    const int r = run_tree(c);
+    if (r < 0) return -10;
+    if (r == 1) {
+      c->inited = true;
+      fill_stats(c, st);
+      return 0;
     }
   }
   if (!run_init(c)) return -10;

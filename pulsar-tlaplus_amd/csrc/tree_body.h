@@ -1,13 +1,19 @@
 // pulsar-tlaplus_amd/csrc/tree_body.h -- device body of the component-tree
-// engine (tree.h), shared by the precompiled kernel (tree.hip) and the
-// run-time specialized one (jit.cpp): a wavefront runs G components of a
-// layer at once, one per group of 64 / G lanes, each with its FPSet in LDS;
-// a component's BFS is a multi-source BFS whose sources are its parent
-// component's states with the component's message appended.  L is the
-// runtime layout (precompiled kernel) or a constexpr one (jit.cpp), in which
-// case every field folds.
+// engine (tree.h), shared by the precompiled kernels (tree.hip) and the
+// run-time specialized ones (jit.cpp): a wavefront runs G components at once,
+// one per group of 64 / G lanes, each with its FPSet in LDS.
+//   - Producer modelled (CLOSED = false): a component's BFS is a multi-source
+//     BFS whose sources are its parent component's states with the
+//     component's message appended; states are 32-bit local keys.
+//   - Closed (CLOSED = true: no Producer, components too large for a lane of
+//     the component engine): a component is the closure of one initial state,
+//     states are component codes (component_code.h) and words of type W
+//     (u64, or u128 for a > 63-bit layout).
+// L is the runtime layout (precompiled kernels) or a constexpr one (jit.cpp),
+// in which case every field folds.
 #pragma once
 #if !defined(__HIPCC_RTC__)
+#include "component_code.h"
 #include "component_model.h"
 #include "kernels.h"
 #include "tree.h"
@@ -16,15 +22,16 @@
 namespace tlcg {
 
 // CAP states per component, T FPSet slots (a power of 2, load <= CAP / T),
-// G components per wavefront.  A component's depth holds ~16 states, so one
-// component per 64-lane wavefront leaves most lanes idle and pays the
-// scalar (exec-mask, loop) instructions once per state; G groups share them.
-template <int CAP, int T, int G>
+// G components per wavefront.  A component's depth holds ~16 states (P8) or
+// fewer, so one component per 64-lane wavefront leaves most lanes idle and
+// pays the scalar (exec-mask, loop) instructions once per state; G groups
+// share them.
+template <int CAP, int T, int G, bool CLOSED = false, typename W = u64>
 __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   constexpr int S = 64 / G;  // lanes per group
   static_assert((T & (T - 1)) == 0 && T >= CAP, "T: a power of 2 >= CAP");
-  __shared__ uint32_t h[G][T];       // local key + 1, 0 = empty
-  __shared__ uint32_t keys[G][CAP];  // each component's local keys in BFS (depth) order
+  __shared__ uint32_t h[G][T];       // key + 1, 0 = empty
+  __shared__ uint32_t keys[G][CAP];  // each component's keys in BFS (depth) order
   __shared__ unsigned long long lvl_d[TREE_MAXLV], lvl_g[TREE_MAXLV];
   const int lane = threadIdx.x;
   const int g = lane / S, sub = lane % S;
@@ -41,19 +48,22 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   u64 ci = (u64)blockIdx.x * G + (u64)g;
   const u64 cstep = (u64)gridDim.x * G;
   bool have = false;
-  u64 np = 0, pc = 0, e = 0, msgs = 0;
+  u64 np = 0, pc = 0, e = 0;
+  W msgs = 0;
   int j = 0, nprod = 0, n = 0, f0 = 0, d = 0;
   CompMsgs cm{};
+  CodeConsts kc{};
   const u64* pst = nullptr;
   const uint8_t* pdep = nullptr;
   u64 pgb = 0, gb = 0;
-  u64 *st = nullptr, *par = nullptr;
+  W* st = nullptr;
+  u64* par = nullptr;
   uint8_t* dp = nullptr;
   uint32_t* hh = &h[g][0];
   uint32_t* kk = &keys[g][0];
   // insert the group's candidates (pred) at depth dd: LDS CAS on the key, the
   // new ones appended in lane order
-  auto insert = [&](bool pred, lkey key, u64 pref, int dd) {
+  auto insert = [&](bool pred, uint32_t key, u64 pref, int dd) {
     bool isnew = false;
     if (pred) {
       unsigned s = (key * 0x9E3779B1u) >> (32 - log2t);
@@ -74,10 +84,15 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     } else if (isnew) {
       const int pos = n + __popcll(m & below);
       kk[pos] = key;
-      st[pos] = msgs | ((u64)key << mb);
       par[pos] = pref == NO_PARENT ? NO_PARENT : (a.rank_tag | pref);
-      dp[pos] = (uint8_t)dd;
-      if (check_invariants_k(L, cm, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
+      if constexpr (CLOSED) {
+        st[pos] = code_word<W>(L, kc, msgs, key);
+        if (check_invariants_cb(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
+      } else {
+        st[pos] = msgs | ((u64)key << mb);
+        dp[pos] = (uint8_t)dd;  // (read by the next layer)
+        if (check_invariants_k(L, cm, key) >= 0) flags |= TREE_EVENT;
+      }
     }
     n = n + cnt > CAP ? CAP : n + cnt;
   };
@@ -85,25 +100,34 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     // a group without a component takes its next one
     if (!have && ci < a.n_comp) {
       for (int i = sub * 4; i < T; i += S * 4) *reinterpret_cast<uint4*>(&hh[i]) = make_uint4(0, 0, 0, 0);
-      if (a.layer == 0) {
-        np = a.n_init;
-        pc = 0;
-        j = 0;
+      if constexpr (CLOSED) {
+        np = 1;  // the component's initial state
+        const W s0 = init_state<W>(L, a.comp0 + ci);
+        msgs = s0 & messages_mask<W>(L);
+        cm = comp_msgs_init(L, (u64)s0);  // (`messages` sits in the low word)
+        kc = code_consts(L, cm);
+        if (code_word<W>(L, kc, msgs, code_encode_w<W>(L, s0)) != s0) flags |= TREE_OVERFLOW;  // no code
       } else {
-        pc = ci / (u64)L.nkv;
-        j = (int)(ci % (u64)L.nkv);
-        np = a.par_n[pc];
+        if (a.layer == 0) {
+          np = a.n_init;
+          pc = 0;
+          j = 0;
+        } else {
+          pc = ci / (u64)L.nkv;
+          j = (int)(ci % (u64)L.nkv);
+          np = a.par_n[pc];
+        }
+        pst = a.layer ? a.par_states + pc * CAP : nullptr;
+        pdep = a.layer ? a.par_dep + pc * CAP : nullptr;
+        pgb = a.par_gbase + pc * CAP;
+        const u64 w0 = a.layer == 0 ? init_state(L, 0) : producer_succ(L, pst[0], a.layer - 1, j);
+        msgs = (W)(w0 & L.msgs_mask);
+        cm = comp_msgs_init(L, w0);        // everything that reads only `messages`
+        nprod = cm.len < L.N ? L.nkv : 0;  // Producer's successors (into the children)
+        dp = a.dep + ci * CAP;
       }
-      pst = a.layer ? a.par_states + pc * CAP : nullptr;
-      pdep = a.layer ? a.par_dep + pc * CAP : nullptr;
-      pgb = a.par_gbase + pc * CAP;
-      const u64 w0 = a.layer == 0 ? init_state(L, 0) : producer_succ(L, pst[0], a.layer - 1, j);
-      msgs = w0 & L.msgs_mask;
-      cm = comp_msgs_init(L, w0);  // everything that reads only `messages`
-      nprod = cm.len < L.N ? L.nkv : 0;  // Producer's successors (into the children)
-      st = a.states + ci * CAP;
+      st = reinterpret_cast<W*>(a.states) + ci * CAP;
       par = a.parents + ci * CAP;
-      dp = a.dep + ci * CAP;
       gb = a.gbase + ci * CAP;
       n = f0 = d = 0;
       e = 0;
@@ -120,7 +144,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         have = false;
         ci += cstep;
       } else {
-        d = a.layer == 0 ? 0 : (int)pdep[e] + 1;
+        d = CLOSED || a.layer == 0 ? 0 : (int)pdep[e] + 1;
       }
     }
     if (have && d >= TREE_MAXLV - 1) flags |= TREE_OVERFLOW;
@@ -129,14 +153,18 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     while (__ballot(more)) {
       const u64 i = e + (u64)sub;
       bool ok = more && i < np;
-      lkey key = 0;
+      uint32_t key = 0;
       u64 pref = NO_PARENT;
-      if (ok && a.layer == 0) {
-        key = (lkey)(init_state(L, i) >> mb);
-      } else if (ok) {
-        ok = (int)pdep[i] + 1 == d;
-        key = (lkey)(producer_succ(L, pst[i], a.layer - 1, j) >> mb);
-        pref = ((pgb + i) << L.ord_bits) | (u64)ordinal_of(L, ACT_PRODUCER, j);
+      if constexpr (CLOSED) {
+        if (ok) key = code_encode_w<W>(L, init_state<W>(L, a.comp0 + ci));
+      } else {
+        if (ok && a.layer == 0) {
+          key = (lkey)(init_state(L, i) >> mb);
+        } else if (ok) {
+          ok = (int)pdep[i] + 1 == d;
+          key = (lkey)(producer_succ(L, pst[i], a.layer - 1, j) >> mb);
+          pref = ((pgb + i) << L.ord_bits) | (u64)ordinal_of(L, ACT_PRODUCER, j);
+        }
       }
       insert(ok, key, pref, d);
       const int taken = __popcll(__ballot(ok) & gmask);
@@ -150,12 +178,19 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     for (int b = f0; __ballot(have && b < f1); b += S) {
       const int i = b + sub;
       const bool ok = have && i < f1;
-      const lkey k = ok ? kk[i] : 0;
-      lkey t = 0, t2 = 0;
-      int act = 0;
-      const int r = ok ? compactor_step_k(L, cm, msgs, k, k_phase(L, k), &t, &act) : 0;
-      const bool crash = ok && crash_step_k(L, k, &t2);
-      const int nsucc = nprod + (r == 1) + (int)crash + selfloop_count_k(L, cm, k);
+      const uint32_t k = ok ? kk[i] : 0;
+      uint32_t t = 0, t2 = 0;
+      int act = 0, r, nsucc;
+      bool crash;
+      if constexpr (CLOSED) {
+        r = ok ? compactor_step_cb(L, kc, k, &t, &act) : 0;
+        crash = ok && crash_step_c(L, k, &t2);
+        nsucc = (r == 1) + (int)crash + selfloop_count_c(L, kc, k);
+      } else {
+        r = ok ? compactor_step_k(L, cm, (u64)msgs, k, k_phase(L, k), &t, &act) : 0;
+        crash = ok && crash_step_k(L, k, &t2);
+        nsucc = nprod + (r == 1) + (int)crash + selfloop_count_k(L, cm, k);
+      }
       if (ok) {
         gen += (u64)nsucc;
         if (r == 2 || (nsucc == 0 && L.check_deadlock)) flags |= TREE_EVENT;

@@ -59,7 +59,10 @@ def test_golden_case(case, mode):
         g = GOLDEN[case]["result"]
         per_component = g["distinct"] // tlcgpu.init_count(m)
         fits = per_component <= 255 and g["depth"] <= 47 and component_key_fits(c)
-        assert r.engine == ("component" if fits else "global"), (r.engine, per_component)
+        # a component too large for a lane goes to the component tree's closed
+        # mode when its codes fit (csrc/tree.h), else to the global engine
+        tree = code_bits(c) <= 31 and per_component <= 2048 and g["depth"] <= 126
+        assert r.engine == ("component" if fits else "tree" if tree else "global"), (r.engine, per_component)
 
 
 ERROR_CASES = [c for c in FULL_CASES if GOLDEN[c]["result"]["result"] != "ok"]
@@ -131,6 +134,13 @@ def component_key_fits(c):
     led_sh = c["N"].bit_length() + c["N"] * ((nk - 1).bit_length() + (nv - 1).bit_length())
     bits = tlcgpu.state_bits(m)
     return bits <= 63 and bits - led_sh <= 32 and c["N"] <= 8
+
+
+def code_bits(c):
+    """bits of a component code (csrc/component_code.h): C presence bits, 5
+    (readPosition, horizon, phase), context and cursor context, 2 (cursor
+    present, cursor horizon), crash count"""
+    return c["C"] + 7 + 2 * c["C"].bit_length() + c["K"].bit_length()
 
 
 def want_ok(case):
@@ -277,16 +287,19 @@ def test_component_cascade(case, monkeypatch):
     check_against_golden(case, r, False)
 
 
-def test_g9deep_scaled_counts():
+@pytest.mark.parametrize("engine", ["auto", "global"])
+def test_g9deep_scaled_counts(engine):
     """KeySpace = ValueSpace = 1..10, CompactionTimesLimit
-    = 12 -> a 93-bit state (two words, the wide FPSet): 11^6 x 557 =
-    986,759,477 distinct, 1,119,626,552 generated, depth 74."""
+    = 12 -> a 93-bit state (two words): 11^6 x 557 = 986,759,477 distinct,
+    1,119,626,552 generated, depth 74 -- on the component tree's closed mode
+    (auto: 557-state components on 28-bit codes) and on the wide FPSet."""
     m = tlcgpu.Model(compaction_times_limit=12, **M8)
     assert tlcgpu.state_words(m) == 2
-    r = tlcgpu.run(m, log2_fpset_slots=31, state_capacity=1_000_000_000)
+    kw = dict(log2_fpset_slots=31, state_capacity=1_000_000_000) if engine == "global" else {}
+    r = tlcgpu.run(m, engine=engine, **kw)
     per_m_law("G9deep_first_M", 11 ** 6, r)
     assert (r.distinct, r.generated, r.depth) == (986_759_477, 1_119_626_552, 74)
-    assert r.engine == "global"
+    assert r.engine == ("tree" if engine == "auto" else "global")
 
 
 
