@@ -249,6 +249,51 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
  * order; the counterexample is that state followed by stuttering), -1 when
  * the property holds, < -1 on a bad model. */
 int64_t tlcg_host_termination_counterexample(const tlcg_model* m);
+/* ---- liveness: PROPERTY Termination (compaction.tla:303-307) on the GPU ----
+ * <- TLC's liveness checker (tlc2.tool.liveness.LiveCheck / LiveWorker) for
+ * Termination == <>P, P the guard of Terminating (compaction.tla:205-214).
+ * The check walks G' = the states reachable from Init through not-P states
+ * (the consistent part of the product with the tableau of []~P):
+ *   TLCG_FAIR_NONE     Spec (compaction.tla:233): every behavior may stutter
+ *                      forever, so <>P fails iff G' is not empty;
+ *   TLCG_FAIR_WF_NEXT  Spec /\ WF_vars(Next) (SF_vars(Next) is the same
+ *                      check): <>P fails iff G' holds a state where
+ *                      <<Next>>_vars is disabled (TLCG_LIVE_STUTTERING) or a
+ *                      cycle of non-stuttering steps (TLCG_LIVE_CYCLE, found by
+ *                      peeling G' in Kahn order on the GPU).
+ * The counterexample goes to states[0..*len) (tlcg_state_words uint64s
+ * each) with the actions into them (TLCG_ACT_INIT first); it ends stuttering
+ * (loop_to = -1) or steps back to states[loop_to] by back_action.  Which of
+ * several counterexamples TLC prints is [TLC-ext]: this returns, without
+ * fairness, the first not-P initial state in Init order; with fairness, the
+ * least packed state of the shallowest level holding a stuck state, or the
+ * first cycle reached from the shallowest state left after peeling.  The check
+ * allocates its own device buffers (o->state_capacity and
+ * o->log2_fpset_slots size them, grown on demand; o->device). */
+enum { TLCG_FAIR_NONE = 0, TLCG_FAIR_WF_NEXT = 1 };
+enum { TLCG_LIVE_HOLDS = 0, TLCG_LIVE_STUTTERING = 1, TLCG_LIVE_CYCLE = 2 };
+typedef struct tlcg_liveness {
+  int32_t holds;          /* 1: every behavior (fair behavior) reaches P */
+  int32_t kind;           /* TLCG_LIVE_* */
+  int32_t fairness;       /* TLCG_FAIR_* checked */
+  int32_t depth;          /* BFS levels of G' */
+  uint64_t states_notp;   /* |G'| */
+  uint64_t init_notp;     /* initial states in G' */
+  uint64_t edges_notp;    /* non-stuttering transitions into states of G' (from states of G') */
+  uint64_t stuck;         /* states of G' where a (fair) behavior may stutter forever */
+  uint64_t on_cycles;     /* states of G' left after peeling: on a cycle or reachable from one */
+  uint64_t peel_rounds;   /* Kahn rounds */
+  int32_t trace_len;      /* states in the counterexample (0 when it holds) */
+  int32_t loop_to;        /* -1: the counterexample ends stuttering; else its back-edge target */
+  int32_t back_action;    /* TLCG_ACT_* of the back edge (loop_to >= 0) */
+  int32_t reserved;
+  double kernel_ms;       /* device time of the BFS and peeling kernels (HIP events) */
+  double wall_ms;         /* whole call */
+} tlcg_liveness;
+int tlcg_check_termination(const tlcg_model* m, const tlcg_opts* o, int32_t fairness, tlcg_liveness* out,
+                           uint64_t* states, int32_t* actions, int32_t cap, int32_t* len, char* err,
+                           int32_t err_cap);
+
 /* Enable xGMI peer access among devices 0..n-1 (one process driving contexts
  * on several devices, e.g. tlc-hip -gpus N).  Returns the pairs enabled. */
 int tlcg_peer_access(int32_t n);

@@ -285,3 +285,74 @@ class Model:
         hist = [outdeg.get(i, 0) for i in range(max(outdeg) + 1)] if outdeg else []
         return dict(result="ok", generated=generated, distinct=len(states), depth=len(levels), levels=levels,
                     outdegree=hist)
+
+    # ---- PROPERTY Termination, compaction.tla:303-307 ----
+    def termination_p(self, s):
+        """Termination's state predicate P (<>P), the guard of Terminating."""
+        msgs, led, cur, ph, p1r, hz, ctx, crash, cons = s
+        return (len(msgs) == self.N and ph == W and self.max_ledger(led) == self.C
+                and (not self.consumer or cons == self.ctl))
+
+    def liveness(self, fair):
+        """<>P under Spec (fair=False: every behavior may stutter forever) or
+        Spec /\\ WF_vars(Next) (fair=True).  Counterexamples live in G', the
+        states reachable from Init through not-P states.  Under WF a behavior
+        stutters forever only where every successor equals the state ("stuck"),
+        else it takes non-stuttering steps forever: <>P fails iff G' has a stuck
+        state or a cycle.  The cycle test here is a depth-first search for a
+        back edge (white/grey/black colouring) -- a third algorithm beside the C
+        oracle's Tarjan SCC and the GPU's Kahn peeling."""
+        index, states, depth, adj = {}, [], [], []
+        q = deque()
+        for t in self.inits():
+            if not self.termination_p(t) and t not in index:
+                index[t] = len(states)
+                states.append(t)
+                depth.append(1)
+                q.append(index[t])
+        edges, stuck, stuck_depth = 0, 0, None
+        while q:
+            k = q.popleft()
+            s = states[k]
+            moves, out = 0, []
+            for _, t in self.successors(s):
+                if t == s:
+                    continue  # a stutter
+                moves += 1
+                if self.termination_p(t):
+                    continue
+                if t not in index:
+                    index[t] = len(states)
+                    states.append(t)
+                    depth.append(depth[k] + 1)
+                    q.append(index[t])
+                out.append(index[t])
+            edges += len(out)
+            adj.append(out)
+            if moves == 0 or not fair:
+                stuck += 1
+                if stuck_depth is None:
+                    stuck_depth = depth[k]
+        colour = [0] * len(states)  # 0 white, 1 grey (on the DFS path), 2 black
+        cyclic = False
+        for r in range(len(states)):
+            if colour[r] or cyclic:
+                continue
+            stack = [(r, 0)]
+            colour[r] = 1
+            while stack and not cyclic:
+                v, i = stack[-1]
+                if i < len(adj[v]):
+                    stack[-1] = (v, i + 1)
+                    w = adj[v][i]
+                    if colour[w] == 1:
+                        cyclic = True
+                    elif colour[w] == 0:
+                        colour[w] = 1
+                        stack.append((w, 0))
+                else:
+                    colour[v] = 2
+                    stack.pop()
+        return dict(holds=stuck == 0 and not cyclic, states_notp=len(states),
+                    init_notp=sum(1 for d in depth if d == 1), edges_notp=edges, stuck=stuck,
+                    stuck_min_depth=stuck_depth or 0, cyclic=cyclic)

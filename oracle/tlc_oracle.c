@@ -41,6 +41,7 @@
  * Usage: tlc_oracle -N 3 -C 3 -K 1 -keys 1,2 -values 1,2 [-retain 1]
  *        [-producer 0] [-consumer 0] [-ctl 2] [-inv TypeSafe,...]
  *        [-nodeadlock] [-init-lo A -init-hi B] [-levels] [-quiet]
+ *        [-liveness none|wf]   (PROPERTY Termination instead of the safety check)
  * Prints one JSON object on stdout.
  */
 #include <stdint.h>
@@ -542,10 +543,170 @@ static int parse_list(const char *a, int *out, int max) {
 
 static int cmp_int(const void *a, const void *b) { return (*(const int *)a > *(const int *)b) - (*(const int *)a < *(const int *)b); }
 
+/* Initial state number idx of Init (compaction.tla:188-202), TLC order */
+static void init_state_idx(St *s, long long idx) {
+  init_state(s);
+  if (PRODUCER) return;
+  s->nmsg = N;
+  for (int i = 0; i < N; i++) {
+    int d = (int)(idx % (nKeySet * nValueSet)); idx /= (nKeySet * nValueSet);
+    s->msgs[i].id = i + 1; s->msgs[i].key = KeySet[d % nKeySet]; s->msgs[i].value = ValueSet[d / nKeySet];
+  }
+}
+
+/* All successors of s under Next (compaction.tla:216-231), stutters
+   included; returns the count, or -1 on an evaluation error. */
+static int next_all(const St *s, St *out) {
+  int n = 0;
+  for (int a = 0; a < N_ACTIONS; a++) {
+    int cnt = 0, rc = EV_FALSE;
+    St *o = out + n;
+    switch (a) {
+      case A_PRODUCER: if (PRODUCER) rc = act_producer(s, o, &cnt); break;
+      case A_PHASEONE: rc = act_phase_one(s, o); cnt = rc == EV_TRUE; break;
+      case A_WRITE: rc = act_write(s, o); cnt = rc == EV_TRUE; break;
+      case A_UCTX: rc = act_update_context(s, o); cnt = rc == EV_TRUE; break;
+      case A_UHOR: rc = act_update_horizon(s, o); cnt = rc == EV_TRUE; break;
+      case A_PERSIST: rc = act_persist(s, o); cnt = rc == EV_TRUE; break;
+      case A_DELETE: rc = act_delete(s, o); cnt = rc == EV_TRUE; break;
+      case A_CRASH: rc = act_crash(s, o); cnt = rc == EV_TRUE; break;
+      case A_CONSUMER: if (CONSUMER) { o[0] = *s; cnt = 1; } break;
+      case A_TERMINATING: if (enabled_terminating(s)) { o[0] = *s; cnt = 1; } break;
+    }
+    if (rc == EV_ERROR) return -1;
+    n += cnt;
+  }
+  return n;
+}
+
+static int same_state(const St *a, const St *b) {
+  int32_t x[1024], y[1024];
+  int n = serialize(a, x), m = serialize(b, y);
+  return n == m && memcmp(x, y, n * sizeof(int32_t)) == 0;
+}
+
+/* ---------------- liveness: PROPERTY Termination ----------------
+   Termination == <>P, compaction.tla:303-307; P is the guard of Terminating
+   (enabled_terminating).  A behavior of the spec violates <>P iff it never
+   reaches a P state, so the counterexamples live in G' = the states reachable
+   from Init through not-P states only (tlc2.tool.liveness builds the product
+   of the state graph with the tableau of []~P, which is exactly G').
+   Fairness `fair`:
+     0  Spec (compaction.tla:233), no fairness: every behavior may stutter
+        forever, so every state of G' ends a counterexample;
+     1  Spec /\ WF_vars(Next): a fair behavior stutters forever only in a state
+        where <<Next>>_vars is disabled (no successor different from the state)
+        and otherwise takes infinitely many non-stuttering steps, so <>P fails
+        iff G' holds such a "stuck" state or a cycle of non-stuttering steps
+        (an SCC of G' with more than one state; self-loops are stutters).
+   This restatement builds G' explicitly and runs Tarjan's SCC algorithm on
+   it (iteratively); the product's GPU path peels G' instead (Kahn), so the
+   two are independent.  Prints one JSON object. */
+static uint64_t *lv_src, *lv_dst, lv_ne, lv_cap;
+static void lv_edge(uint64_t a, uint64_t b) {
+  if (lv_ne == lv_cap) {
+    lv_cap = lv_cap ? lv_cap * 2 : 1 << 16;
+    lv_src = realloc(lv_src, lv_cap * sizeof *lv_src); lv_dst = realloc(lv_dst, lv_cap * sizeof *lv_dst);
+    if (!lv_src || !lv_dst) { fprintf(stderr, "oom\n"); exit(3); }
+  }
+  lv_src[lv_ne] = a; lv_dst[lv_ne] = b; lv_ne++;
+}
+
+static int run_liveness(int fair) {
+  static St succ[MAXK * MAXK + 16];
+  fp_grow();
+  long long total = 1;
+  if (!PRODUCER) for (int i = 0; i < N; i++) total *= (long long)(nKeySet * nValueSet);
+  uint64_t *depth = NULL, dcap = 0;
+  for (long long idx = 0; idx < total; idx++) {
+    St s; init_state_idx(&s, idx);
+    if (enabled_terminating(&s)) continue;
+    uint64_t k; fp_put(&s, -1, A_INIT, &k);
+  }
+  uint64_t n_init = n_states, stuck = 0, first_stuck = ~0ull;
+  int error = 0;
+  for (uint64_t h = 0; h < n_states && !error; h++) {
+    St s; load_state(h, &s);
+    int n = next_all(&s, succ);
+    if (n < 0) { error = 1; break; }
+    int moves = 0;
+    for (int j = 0; j < n; j++) {
+      if (same_state(&succ[j], &s)) continue;  /* a stutter */
+      moves++;
+      if (enabled_terminating(&succ[j])) continue;  /* P reached */
+      uint64_t k; fp_put(&succ[j], (int64_t)h, A_INIT, &k);
+      lv_edge(h, k);
+    }
+    if (moves == 0 || fair == 0) { stuck++; if (first_stuck == ~0ull) first_stuck = h; }
+  }
+  /* BFS depth of every state of G' (parents are BFS parents) */
+  dcap = n_states; depth = malloc((dcap + 1) * sizeof *depth);
+  for (uint64_t k = 0; k < n_states; k++) depth[k] = st_parent[k] < 0 ? 1 : depth[st_parent[k]] + 1;
+  /* Tarjan's SCC, iterative, over the CSR form of the edges */
+  uint64_t n = n_states, *off = calloc(n + 1, sizeof *off), *adj = malloc((lv_ne + 1) * sizeof *adj);
+  for (uint64_t e = 0; e < lv_ne; e++) off[lv_src[e] + 1]++;
+  for (uint64_t v = 0; v < n; v++) off[v + 1] += off[v];
+  uint64_t *fill = malloc((n + 1) * sizeof *fill);
+  memcpy(fill, off, (n + 1) * sizeof *fill);
+  for (uint64_t e = 0; e < lv_ne; e++) adj[fill[lv_src[e]]++] = lv_dst[e];
+  int64_t *index = malloc((n + 1) * sizeof *index), *low = malloc((n + 1) * sizeof *low);
+  uint64_t *stack = malloc((n + 1) * sizeof *stack), *cs = malloc((n + 1) * sizeof *cs), *ce = malloc((n + 1) * sizeof *ce);
+  char *on = calloc(n + 1, 1);
+  for (uint64_t v = 0; v < n; v++) index[v] = -1;
+  int64_t next_index = 0; uint64_t sp = 0, big_sccs = 0, cyc_states = 0, first_cycle = ~0ull;
+  for (uint64_t r = 0; r < n; r++) {
+    if (index[r] >= 0) continue;
+    uint64_t csp = 0;
+    cs[csp] = r; ce[csp] = off[r]; csp++;
+    index[r] = low[r] = next_index++; stack[sp++] = r; on[r] = 1;
+    while (csp) {
+      uint64_t v = cs[csp - 1];
+      if (ce[csp - 1] < off[v + 1]) {
+        uint64_t w = adj[ce[csp - 1]++];
+        if (index[w] < 0) {
+          index[w] = low[w] = next_index++; stack[sp++] = w; on[w] = 1;
+          cs[csp] = w; ce[csp] = off[w]; csp++;
+        } else if (on[w] && index[w] < low[v]) low[v] = index[w];
+      } else {
+        if (low[v] == index[v]) {
+          uint64_t size = 0, mn = ~0ull, w;
+          do { w = stack[--sp]; on[w] = 0; size++; if (w < mn) mn = w; } while (w != v);
+          if (size > 1) { big_sccs++; cyc_states += size; if (mn < first_cycle) first_cycle = mn; }
+        }
+        csp--;
+        if (csp) { uint64_t u = cs[csp - 1]; if (low[v] < low[u]) low[u] = low[v]; }
+      }
+    }
+  }
+  int holds = !error && stuck == 0 && big_sccs == 0;
+  printf("{\"liveness\": \"Termination\", \"fairness\": \"%s\", \"holds\": %s, \"error\": %s, "
+         "\"states_notp\": %llu, \"init_notp\": %llu, \"edges_notp\": %llu, \"stuck\": %llu, "
+         "\"stuck_min_depth\": %llu, \"cyclic_sccs\": %llu, \"cyclic_states\": %llu",
+         fair ? "WF_vars(Next)" : "none", holds ? "true" : "false", error ? "true" : "false",
+         (unsigned long long)n, (unsigned long long)n_init, (unsigned long long)lv_ne, (unsigned long long)stuck,
+         (unsigned long long)(first_stuck == ~0ull ? 0 : depth[first_stuck]), (unsigned long long)big_sccs,
+         (unsigned long long)cyc_states);
+  if (first_stuck != ~0ull) {
+    /* the shallowest stuck state (BFS order) and its path from Init */
+    printf(", \"stuck_trace\": [");
+    int64_t chain[4096]; int nc = 0;
+    for (int64_t k = (int64_t)first_stuck; k >= 0 && nc < 4096; k = st_parent[k]) chain[nc++] = k;
+    for (int i = nc - 1; i >= 0; i--) {
+      St s; load_state((uint64_t)chain[i], &s);
+      printf("%s", i == nc - 1 ? "" : ", ");
+      print_state_json(stdout, &s);
+    }
+    printf("]");
+  }
+  printf("}\n");
+  free(off); free(adj); free(fill); free(index); free(low); free(stack); free(cs); free(ce); free(on); free(depth);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   int keys[MAXK], nkeys = 0, vals[MAXK], nvals = 0;
   long long init_lo = 0, init_hi = -1;
-  int print_levels = 0, want_trace = 1;
+  int print_levels = 0, want_trace = 1, liveness = -1;
   char invs[512] = "TypeSafe,CompactionHorizonCorrectness";
   for (int i = 1; i < argc; i++) {
     const char *a = argv[i];
@@ -565,6 +726,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "-init-hi")) init_hi = atoll(NEXT);
     else if (!strcmp(a, "-levels")) print_levels = 1;
     else if (!strcmp(a, "-notrace")) want_trace = 0;
+    else if (!strcmp(a, "-liveness")) { const char *f = NEXT; liveness = !strcmp(f, "wf") ? 1 : 0; }
     else { fprintf(stderr, "unknown arg %s\n", a); return 2; }
   }
   if (N < 0 || N > MAXN || C < 0 || C > MAXC || K < 0) { fprintf(stderr, "constants out of oracle range\n"); return 2; }
@@ -584,6 +746,8 @@ int main(int argc, char **argv) {
       Inv[nInv++] = k;
     }
   }
+
+  if (liveness >= 0) return run_liveness(liveness);
 
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);

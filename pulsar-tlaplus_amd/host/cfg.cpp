@@ -396,7 +396,7 @@ static bool invariant_matches(const Module& m, const std::string& name) {
 }
 
 bool bind_model(const Config& cfg, const Module& mod, bool deadlock_flag, tlcg_model* m, std::string* err,
-                int* exit_code) {
+                int* exit_code, int* fairness) {
   *m = tlcg_model();
   *exit_code = 150;  // [TLC-ext] configuration/semantic error
   static const char* kParams[] = {"MessageSentLimit", "CompactionTimesLimit", "ModelConsumer", "ConsumeTimesLimit",
@@ -515,12 +515,29 @@ bool bind_model(const Config& cfg, const Module& mod, bool deadlock_flag, tlcg_m
     return false;
   }
   // ---- behaviour spec ----
-  if (!cfg.specification.empty()) {
-    if (cfg.specification != "Spec") {
-      *err = "Error: this checker supports SPECIFICATION Spec (compaction.tla:233) only.";
+  if (fairness) *fairness = TLCG_FAIR_NONE;
+  if (!cfg.specification.empty() && cfg.specification != "Spec") {
+    // a fair specification the user adds to the module: Spec (compaction.tla:233)
+    // conjoined with weak or strong fairness of Next; both ask that a
+    // behavior never stutters forever where <<Next>>_vars is enabled, which is
+    // the one property liveness checking needs from them (tlcg_check_termination)
+    const Def* d = mod.find(cfg.specification);
+    std::string body;
+    if (d) {
+      const size_t eq = d->norm.find("==");
+      for (char ch : d->norm.substr(eq == std::string::npos ? 0 : eq + 2))
+        if (!isspace((unsigned char)ch)) body += ch;
+    }
+    static const char* kFair[] = {"Spec/\\WF_vars(Next)", "Spec/\\SF_vars(Next)",
+                                  "Init/\\[][Next]_vars/\\WF_vars(Next)", "Init/\\[][Next]_vars/\\SF_vars(Next)"};
+    const bool fair = d && std::find(std::begin(kFair), std::end(kFair), body) != std::end(kFair);
+    if (!fair) {
+      *err = "Error: this checker supports SPECIFICATION Spec (compaction.tla:233), or a definition Spec /\\ "
+             "WF_vars(Next) (or SF_vars(Next)), only.";
       return false;
     }
-  } else if (cfg.init != "Init" || cfg.next != "Next") {
+    if (fairness) *fairness = TLCG_FAIR_WF_NEXT;
+  } else if (cfg.specification.empty() && (cfg.init != "Init" || cfg.next != "Next")) {
     *err = "Error: the configuration needs SPECIFICATION Spec or INIT Init / NEXT Next.";
     return false;
   }

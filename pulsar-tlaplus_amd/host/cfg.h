@@ -65,7 +65,9 @@ bool recognize_compaction(const Module& m, std::string* err);
 
 // Binds cfg constants to the model (ASSUME of compaction.tla:25-35 included).
 // On failure `err` carries TLC-style text and `exit_code` TLC's exit status.
+// `fairness` (may be null) gets the SPECIFICATION's fairness: TLCG_FAIR_NONE
+// for Spec, TLCG_FAIR_WF_NEXT for a module definition Spec /\ WF_vars(Next).
 bool bind_model(const Config& cfg, const Module& mod, bool deadlock_flag, tlcg_model* m, std::string* err,
-                int* exit_code);
+                int* exit_code, int* fairness = nullptr);
 
 }  // namespace tlchost

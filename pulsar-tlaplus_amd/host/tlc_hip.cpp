@@ -192,8 +192,8 @@ int main(int argc, char** argv) {
   std::printf("Semantic processing of module %s\n", mod.name.c_str());
   std::printf("Starting... (%s)\n", now_str().c_str());
   tlcg_model model;
-  int code = 0;
-  if (!bind_model(cfg, mod, o.deadlock_off, &model, &err, &code)) {
+  int code = 0, fairness = TLCG_FAIR_NONE;
+  if (!bind_model(cfg, mod, o.deadlock_off, &model, &err, &code, &fairness)) {
     std::printf("%s\n", err.c_str());
     std::printf("Finished in %s at (%s)\n", duration_str(0).c_str(), now_str().c_str());
     return code;
@@ -280,22 +280,49 @@ int main(int argc, char** argv) {
   int rc = 0;
   uint64_t stop_left = ~0ull;  // TLC's "states left on queue" at an error (tlcg_tlc_stop_stats)
   // PROPERTY Termination, checked like TLC after the safety search of the
-  // complete state space ([TLC-ext] message text)
-  int64_t live_idx = -1;
+  // complete state space ([TLC-ext] message text), on the GPU
+  // (tlcg_check_termination: the not-P part of the state graph, its stuck
+  // states and, under fairness, its cycles)
+  bool live_fail = false;
   if (st.status == TLCG_DONE && !cfg.properties.empty()) {
     std::printf("Checking temporal properties for the complete state space with %llu total distinct states at (%s)\n",
                 (unsigned long long)st.distinct, now_str().c_str());
-    live_idx = tlcg_host_termination_counterexample(&model);
+    const int words = tlcg_state_words(&model);
+    std::vector<uint64_t> lstates((size_t)words << 16);
+    std::vector<int32_t> lacts(1 << 16);
+    int32_t ln = 0;
+    tlcg_liveness lv;
+    tlcg_opts lo = opts;
+    lo.state_capacity = st.distinct;  // G' is a subset of the reachable states
+    lo.log2_fpset_slots = 0;
+    char lerr[512] = {0};
+    // (the check allocates its own device buffers, about 64 B per not-P state,
+    // beside the safety run's, which the outdegree statistics below still read)
+    if (tlcg_check_termination(&model, &lo, fairness, &lv, lstates.data(), lacts.data(), (int32_t)lacts.size(), &ln,
+                               lerr, (int32_t)sizeof lerr) != 0) {
+      std::printf("Error: the liveness check failed: %s\n", lerr);
+      std::printf("Finished in %s at (%s)\n", duration_str(0).c_str(), now_str().c_str());
+      return 255;
+    }
+    std::printf("Finished checking temporal properties in %s at %s\n", duration_str(lv.wall_ms / 1000.0).c_str(),
+                now_str().c_str());
+    if (!lv.holds) {
+      live_fail = true;
+      std::vector<char> buf(1 << 16);
+      std::printf("Error: Temporal properties were violated.\n\n");
+      std::printf("Error: The following behavior constitutes a counter-example:\n\n");
+      for (int i = 0; i < ln; ++i) {
+        if (lacts[(size_t)i] < 0) std::printf("State %d: <Initial predicate>\n", i + 1);
+        else std::printf("State %d: <%s>\n", i + 1, action_location(mod, lacts[(size_t)i]).c_str());
+        tlcg_decode_words(&model, &lstates[(size_t)i * words], buf.data(), (int32_t)buf.size());
+        std::printf("%s\n\n", buf.data());
+      }
+      if (lv.loop_to < 0) std::printf("State %d: Stuttering\n", ln + 1);
+      else std::printf("State %d: Back to state %d: <%s>\n", ln + 1, lv.loop_to + 1,
+                       action_location(mod, lv.back_action).c_str());
+    }
   }
-  if (live_idx >= 0) {
-    uint64_t s0[2] = {0, 0};
-    std::vector<char> buf(1 << 16);
-    tlcg_host_init_state_words(&model, (uint64_t)live_idx, s0);
-    tlcg_decode_words(&model, s0, buf.data(), (int32_t)buf.size());
-    std::printf("Error: Temporal properties were violated.\n\n");
-    std::printf("Error: The following behavior constitutes a counter-example:\n\n");
-    std::printf("State 1: <Initial predicate>\n%s\n\n", buf.data());
-    std::printf("State 2: Stuttering\n");
+  if (live_fail) {
     rc = 13;
   } else if (st.status == TLCG_DONE) {
     std::printf("Model checking completed. No error has been found.\n");

@@ -57,6 +57,17 @@ class tlcg_stats(C.Structure):
                 ("transport", C.c_uint64)]
 
 
+class tlcg_liveness(C.Structure):
+    _fields_ = [("holds", C.c_int32), ("kind", C.c_int32), ("fairness", C.c_int32), ("depth", C.c_int32),
+                ("states_notp", C.c_uint64), ("init_notp", C.c_uint64), ("edges_notp", C.c_uint64),
+                ("stuck", C.c_uint64), ("on_cycles", C.c_uint64), ("peel_rounds", C.c_uint64),
+                ("trace_len", C.c_int32), ("loop_to", C.c_int32), ("back_action", C.c_int32),
+                ("reserved", C.c_int32), ("kernel_ms", C.c_double), ("wall_ms", C.c_double)]
+
+
+FAIRNESS = {"none": 0, "wf": 1}
+LIVE_KINDS = {0: "holds", 1: "stuttering", 2: "cycle"}
+
 _lib = None
 
 
@@ -125,6 +136,8 @@ def load_library(path: str = LIB_PATH):
         "tlcg_comm_unique_id": (C.c_int, [P, I32]),
         "tlcg_comm_init": (C.c_int, [P, P, I32]),
         "tlcg_run_comm": (C.c_int, [P, S, C.POINTER(U64), I32, C.POINTER(I32)]),
+        "tlcg_check_termination": (C.c_int, [M, O, I32, C.POINTER(tlcg_liveness), C.POINTER(U64),
+                                             C.POINTER(I32), I32, C.POINTER(I32), C.c_char_p, I32]),
         "tlcg_jit_selftest": (C.c_int, [M, C.c_char_p, I32, C.c_char_p, I32][:1] + [C.c_char_p, C.c_char_p, I32]),
     }
     for name, (res, args) in sig.items():
@@ -262,6 +275,51 @@ def host_component_selfcheck(model: Model, first: int, n: int) -> int:
 def host_check_invariants(model: Model, state: int) -> int:
     m = model.to_c()
     return load_library().tlcg_host_check_invariants_words(C.byref(m), _to_words(state, state_words(model)))
+
+
+@dataclass
+class Liveness:
+    """PROPERTY Termination (compaction.tla:303-307) checked on the GPU."""
+    holds: bool
+    kind: str                    # "holds", "stuttering" or "cycle"
+    fairness: str                # "none" (Spec) or "wf" (Spec /\ WF_vars(Next))
+    depth: int                   # BFS levels of G' (the not-P part of the graph)
+    states_notp: int
+    init_notp: int
+    edges_notp: int
+    stuck: int
+    on_cycles: int
+    peel_rounds: int
+    trace: List[Tuple[str, int]] = field(default_factory=list)  # (action into it, state)
+    loop_to: int = -1            # -1: the counterexample ends stuttering
+    back_action: Optional[str] = None
+    kernel_ms: float = 0.0
+    wall_ms: float = 0.0
+
+
+def check_termination(model: Model, fairness: str = "none", device: int = 0, state_capacity: int = 0,
+                      log2_fpset_slots: int = 0) -> Liveness:
+    """TLC's liveness check of PROPERTY Termination under Spec (fairness
+    "none") or Spec /\ WF_vars(Next) ("wf"), through tlcg_check_termination."""
+    lib = load_library()
+    m = model.to_c()
+    o = tlcg_opts()
+    o.device, o.state_capacity, o.log2_fpset_slots = device, state_capacity, log2_fpset_slots
+    out = tlcg_liveness()
+    w = state_words(model)
+    cap = 1 << 12
+    states = (C.c_uint64 * (cap * w))()
+    acts = (C.c_int32 * cap)()
+    n = C.c_int32(0)
+    err = C.create_string_buffer(512)
+    rc = lib.tlcg_check_termination(C.byref(m), C.byref(o), FAIRNESS[fairness], C.byref(out), states, acts, cap,
+                                    C.byref(n), err, len(err))
+    if rc != 0:
+        raise RuntimeError(f"tlcg_check_termination: {rc}: {err.value.decode()}")
+    trace = [("Init" if acts[i] < 0 else ACTIONS[acts[i]], _from_words(states, i, w)) for i in range(n.value)]
+    return Liveness(bool(out.holds), LIVE_KINDS[out.kind], fairness, out.depth, out.states_notp, out.init_notp,
+                    out.edges_notp, out.stuck, out.on_cycles, out.peel_rounds, trace, out.loop_to,
+                    ACTIONS[out.back_action] if out.loop_to >= 0 else None, out.kernel_ms, out.wall_ms)
 
 
 @dataclass

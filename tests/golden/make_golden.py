@@ -117,6 +117,26 @@ def main():
                 # a level-synchronous checker's counts: the level that found the error finished
                 assert (p["eol_generated"], p["eol_distinct"]) == (r["eol_generated"], r["eol_distinct"]), name
         golden[name] = dict(constants=c, result=r)
+        if "init_range" not in c and r["result"] == "ok":
+            # PROPERTY Termination (compaction.tla:303-307) under Spec and under
+            # Spec /\ WF_vars(Next): the C oracle's Tarjan SCC restatement,
+            # cross-checked against the Python oracle's DFS on small graphs
+            live = {}
+            for fair in ("none", "wf"):
+                out = subprocess.run([ORACLE] + oracle_args(c) + ["-liveness", fair], check=True,
+                                     capture_output=True, text=True).stdout
+                lv = json.loads(out)
+                lv.pop("stuck_trace", None)
+                if lv["states_notp"] < 400000:
+                    pl = PyModel(N=c["N"], C=c["C"], K=c["K"], keys=c["keys"], values=c["values"],
+                                 retain=c["retain"], producer=c["producer"], consumer=c["consumer"],
+                                 ctl=c["ctl"]).liveness(fair == "wf")
+                    assert (pl["holds"], pl["states_notp"], pl["init_notp"], pl["edges_notp"], pl["stuck"],
+                            pl["stuck_min_depth"], pl["cyclic"]) == \
+                           (lv["holds"], lv["states_notp"], lv["init_notp"], lv["edges_notp"], lv["stuck"],
+                            lv["stuck_min_depth"], lv["cyclic_sccs"] > 0), (name, fair, pl, lv)
+                live[fair] = lv
+            golden[name]["liveness"] = live
         print(f"{name:24s} {r['result']:10s} gen={r['generated']} distinct={r.get('distinct')} depth={r.get('depth')}")
     assert golden["S"]["result"]["distinct"] == 45198            # compaction.tla:23
     assert golden["P_published"]["result"]["distinct"] == 253361  # compaction.tla:23

@@ -122,3 +122,20 @@ def test_termination_property_is_accepted(tmp_path):
     # PROPERTY Termination (compaction.tla:303-307) is checked after the safety search
     rc, out = run_cli(tmp_path, numeric_cfg(PROPERTY="Termination"))
     assert "Computing initial states..." in out
+
+
+@needs_ref
+def test_fair_specification_is_accepted(tmp_path):
+    # a module definition FairSpec == Spec /\ WF_vars(Next) added to the spec
+    # selects the liveness check under weak fairness of Next; anything else
+    # stays refused
+    tla = open(TLA).read().rstrip()
+    assert tla.endswith("=")
+    body = tla.rstrip("=").rstrip()
+    fair_tla = body + "\n\nFairSpec == Spec /\\ WF_vars(Next)\n\nOddSpec == Spec /\\ WF_vars(Producer)\n\n" + "=" * 20 + "\n"
+    cfg = numeric_cfg(PROPERTY="Termination").replace("SPECIFICATION Spec", "SPECIFICATION FairSpec")
+    rc, out = run_cli(tmp_path, cfg, tla_text=fair_tla)
+    assert "Computing initial states..." in out
+    cfg = numeric_cfg(PROPERTY="Termination").replace("SPECIFICATION Spec", "SPECIFICATION OddSpec")
+    rc, out = run_cli(tmp_path, cfg, tla_text=fair_tla)
+    assert "supports SPECIFICATION Spec" in out and rc == 150

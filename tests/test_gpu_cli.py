@@ -135,3 +135,26 @@ def test_cli_shipped_string_keys_assume(tmp_path):
     assert "Evaluating assumption line 25, col 8 to line 35, col 35 of module compaction failed." in text
     assert 'Attempted to check if the value:\n"key1"\nis an element of Nat.' in text
     assert "Computing initial states..." not in text
+
+
+def test_cli_termination_property(tmp_path):
+    """PROPERTY Termination (compaction.tla:303-307) under Spec: the GPU
+    liveness pass after the safety search; Spec has no fairness, so the
+    counterexample is the first initial state in Init order followed by
+    stuttering, exit code 13 ([TLC-ext] text)"""
+    import tlcgpu
+    from conftest import model_of
+    want = GOLDEN["S"]["result"]
+    rc, lines = run(tmp_path, numeric_cfg(PROPERTY="Termination"))
+    assert rc == 13
+    m = model_of(GOLDEN["S"]["constants"])
+    first = tlcgpu.decode(m, tlcgpu.host_init_state(m, 0)).split("\n")
+    i = lines.index(f"Checking temporal properties for the complete state space with {want['distinct']} total "
+                    f"distinct states at (<DATE>)")
+    assert re.fullmatch(r"Finished checking temporal properties in \d+s at <DATE>", lines[i + 1])
+    assert lines[i + 2:i + 8] == ["Error: Temporal properties were violated.", "",
+                                  "Error: The following behavior constitutes a counter-example:", "",
+                                  "State 1: <Initial predicate>", first[0]]
+    j = i + 7 + len(first)
+    assert lines[i + 8:j] == first[1:] and lines[j:j + 2] == ["", "State 2: Stuttering"]
+    assert f"{want['generated']} states generated, {want['distinct']} distinct states found, 0 states left on queue." in lines
