@@ -43,7 +43,7 @@ def test_abi_version():
 def test_struct_layout_matches_c(tmp_path):
     # every field offset of the ctypes mirrors == what the C compiler lays out
     import subprocess
-    structs = [tlcgpu.tlcg_model, tlcgpu.tlcg_opts, tlcgpu.tlcg_stats]
+    structs = [tlcgpu.tlcg_model, tlcgpu.tlcg_opts, tlcgpu.tlcg_stats, tlcgpu.tlcg_liveness]
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "tlcgpu.h"', "int main(void){"]
     for st in structs:
         src.append(f'printf("%zu\\n", sizeof({st.__name__}));')
