@@ -88,15 +88,39 @@ struct LvBufs {
   LvCtr* ctr;
 };
 
-// Wave-aggregated claim of an index in a counter; all lanes of the wave call it.
-__device__ __forceinline__ u64 wave_claim(bool pred, unsigned long long* ctr) {
-  const u64 m = __ballot(pred);
-  if (m == 0) return 0;
-  const int leader = __ffsll((long long)m) - 1;
-  unsigned long long base = 0;
-  if (__lane_id() == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
-  base = __shfl(base, leader);
-  return base + (u64)__popcll(m & lanemask_lt());
+// Block-aggregated claim of indices in a global counter: one atomic per
+// block per call instead of one per wave (a single counter serializes its
+// atomics).  Every thread of the block calls it (uniform control flow) with
+// NP predicates; at[j] gets the index of each true one, in (wave, j, lane)
+// order.
+template <int NP>
+__device__ __forceinline__ void block_claim(const bool* pred, u64* at, unsigned long long* ctr) {
+  __shared__ unsigned s_wcnt[LV_BLOCK / 64];
+  __shared__ unsigned long long s_base;
+  const int w = (int)(threadIdx.x >> 6);
+  u64 m[NP];
+  unsigned tot = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    m[j] = __ballot(pred[j]);
+    tot += (unsigned)__popcll(m[j]);
+  }
+  if (__lane_id() == 0) s_wcnt[w] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned sum = 0;
+    for (int i = 0; i < LV_BLOCK / 64; ++i) sum += s_wcnt[i];
+    s_base = sum ? atomicAdd(ctr, (unsigned long long)sum) : 0ull;
+  }
+  __syncthreads();
+  u64 base = s_base;
+  for (int i = 0; i < w; ++i) base += s_wcnt[i];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    at[j] = base + (u64)__popcll(m[j] & lanemask_lt());
+    base += (u64)__popcll(m[j]);
+  }
+  __syncthreads();  // (s_wcnt / s_base are reused by the next call)
 }
 
 template <typename W>
@@ -152,8 +176,8 @@ __device__ __forceinline__ u64 lv_lookup(const u64* slots, int log2, W t) {
   return ~0ull;
 }
 
-// insert t (a not-P state) with parent reference pref; every lane of the wave
-// calls it (want = this lane has a state to insert)
+// insert t (a not-P state) with parent reference pref; every thread of the
+// block calls it (want = this lane has a state to insert)
 template <typename W>
 __device__ __forceinline__ void lv_insert(const LvBufs<W>& B, bool want, W t, u64 pref, bool edge) {
   u64 slot = 0;
@@ -164,7 +188,8 @@ __device__ __forceinline__ void lv_insert(const LvBufs<W>& B, bool want, W t, u6
     else if (edge) atomicAdd(&B.indeg[slot], 1u);
   }
   const bool fresh = want && r == 1;
-  const u64 g = wave_claim(fresh, &B.ctr->n);
+  u64 g = 0;
+  block_claim<1>(&fresh, &g, &B.ctr->n);
   if (fresh) {
     if (g >= B.cap) {
       atomicOr(&B.ctr->flags, (unsigned)LV_STORE);
@@ -174,6 +199,94 @@ __device__ __forceinline__ void lv_insert(const LvBufs<W>& B, bool want, W t, u6
       B.slot_of[g] = (u32)slot;
       B.gidx_of[slot] = (u32)g;
     }
+  }
+}
+
+// A batch of up to LV_BATCH candidates of one lane: their first FPSet slots
+// are loaded together (and CASed together where empty), so a lane waits on
+// one scattered round trip per batch instead of one per candidate; collisions
+// go on probing (fpset_put_from).  Wide states take the wave-uniform
+// two-word insert one by one.  slot[j] gets the candidate's slot, fresh[j]
+// whether this lane inserted it.
+constexpr int LV_BATCH = 4;
+template <typename W>
+__device__ __forceinline__ void lv_put_batch(const LvBufs<W>& B, const bool* want, const W* t, u64* slot,
+                                             bool* fresh) {
+  if constexpr (sizeof(W) == 8) {
+    const int sh = 64 - B.log2;
+    const u64 mask = (1ull << B.log2) - 1;
+    u64 v[LV_BATCH];
+#pragma unroll
+    for (int j = 0; j < LV_BATCH; ++j) {
+      slot[j] = mix64((u64)t[j]) >> sh;
+      v[j] = want[j] ? __builtin_nontemporal_load(&B.slots[slot[j]]) : 1;
+    }
+#pragma unroll
+    for (int j = 0; j < LV_BATCH; ++j)
+      if (want[j] && v[j] == 0)
+        v[j] = atomicCAS((unsigned long long*)&B.slots[slot[j]], 0ull, (unsigned long long)((u64)t[j] | SLOT_TAG));
+#pragma unroll
+    for (int j = 0; j < LV_BATCH; ++j) {
+      fresh[j] = false;
+      if (!want[j]) continue;
+      const u64 key = (u64)t[j] | SLOT_TAG;
+      if (v[j] == 0) {
+        fresh[j] = true;
+      } else if (v[j] != key) {
+        const int r = fpset_put_from(B.slots, mask, key, (slot[j] + 1) & mask, &slot[j]);
+        if (r < 0) {
+          atomicOr(&B.ctr->flags, (unsigned)LV_FPSET);
+          slot[j] = ~0ull;
+        }
+        fresh[j] = r == 1;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < LV_BATCH; ++j) {
+      fresh[j] = false;
+      if (!want[j]) continue;
+      const int r = fpset_put<W>(B.slots, B.log2, t[j], mixw<W>(t[j]), &slot[j]);
+      if (r < 0) {
+        atomicOr(&B.ctr->flags, (unsigned)LV_FPSET);
+        slot[j] = ~0ull;
+      }
+      fresh[j] = r == 1;
+    }
+  }
+}
+
+// the same for lookups of states known to be present: first slots together
+template <typename W>
+__device__ __forceinline__ void lv_lookup_batch(const LvBufs<W>& B, const bool* want, const W* t, u64* slot) {
+  if constexpr (sizeof(W) == 8) {
+    const int sh = 64 - B.log2;
+    const u64 mask = (1ull << B.log2) - 1;
+    u64 v[LV_BATCH];
+#pragma unroll
+    for (int j = 0; j < LV_BATCH; ++j) {
+      slot[j] = mix64((u64)t[j]) >> sh;
+      v[j] = want[j] ? B.slots[slot[j]] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < LV_BATCH; ++j) {
+      if (!want[j]) continue;
+      const u64 key = (u64)t[j] | SLOT_TAG;
+      if (v[j] == key) continue;
+      u64 i = slot[j];
+      slot[j] = ~0ull;
+      for (int p = 1; p < MAX_PROBE && v[j] != 0; ++p) {
+        i = (i + 1) & mask;
+        v[j] = B.slots[i];
+        if (v[j] == key) {
+          slot[j] = i;
+          break;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < LV_BATCH; ++j) slot[j] = want[j] ? lv_lookup<W>(B.slots, B.log2, t[j]) : ~0ull;
   }
 }
 
@@ -187,8 +300,10 @@ __global__ __launch_bounds__(LV_BLOCK) void k_lv_init(LvBufs<W> B, u64 n_init) {
     if (i < n_init) {
       s = init_state<W>(B.L, i);
       want = !lv_p(B.L, s);
-      if (want) atomicMin(&B.ctr->first_init, (unsigned long long)i);
     }
+    // the first not-P initial state: the wave's lowest such index, one atomic per wave
+    const u64 wm = __ballot(want);
+    if (wm && __lane_id() == __ffsll((long long)wm) - 1) atomicMin(&B.ctr->first_init, (unsigned long long)i);
     lv_insert(B, want, s, NO_PARENT, false);
   }
 }
@@ -199,31 +314,60 @@ __global__ __launch_bounds__(LV_BLOCK) void k_lv_expand(LvBufs<W> B, u64 a, u64 
   const Layout& L = B.L;
   const int kmax = moves_bound(L);
   const u64 stride = (u64)gridDim.x * LV_BLOCK;
+  // edges and stuck states are summed in registers over the whole loop and
+  // added once per wave at the end (atomics on one counter serialize)
+  u64 edges = 0, nstuck = 0;
+  bool err = false;
   for (u64 base = a + (u64)blockIdx.x * LV_BLOCK; base < b; base += stride) {
     const u64 g = base + threadIdx.x;
     const bool live = g < b;
     const W s = live ? B.store[g] : (W)0;
-    int moves = 0, edges = 0;
-    bool err = false;
-    for (int k = 0; k < kmax; ++k) {
-      W t = 0;
-      int ord = 0, r = 0;
-      if (live) r = lv_move(L, s, k, &t, &ord);
-      if (r == 2) err = true;
-      const bool mv = r == 1;
-      moves += mv;
-      const bool want = mv && !lv_p(L, t);
-      edges += want;
-      lv_insert(B, want, t, (g << L.ord_bits) | (u64)ord, true);
+    int moves = 0;
+    bool serr = false;
+    for (int k0 = 0; k0 < kmax; k0 += LV_BATCH) {
+      W t[LV_BATCH];
+      int ord[LV_BATCH];
+      bool want[LV_BATCH], fresh[LV_BATCH];
+      u64 slot[LV_BATCH];
+#pragma unroll
+      for (int j = 0; j < LV_BATCH; ++j) {
+        t[j] = 0;
+        ord[j] = 0;
+        const int r = live && k0 + j < kmax ? lv_move(L, s, k0 + j, &t[j], &ord[j]) : 0;
+        serr |= r == 2;
+        moves += r == 1;
+        want[j] = r == 1 && !lv_p(L, t[j]);
+        edges += want[j];
+      }
+      lv_put_batch(B, want, t, slot, fresh);
+      u64 ats[LV_BATCH];
+      block_claim<LV_BATCH>(fresh, ats, &B.ctr->n);
+#pragma unroll
+      for (int j = 0; j < LV_BATCH; ++j) {
+        if (want[j] && slot[j] != ~0ull) atomicAdd(&B.indeg[slot[j]], 1u);
+        const u64 at = ats[j];
+        if (fresh[j]) {
+          if (at >= B.cap) {
+            atomicOr(&B.ctr->flags, (unsigned)LV_STORE);
+          } else {
+            B.store[at] = t[j];
+            B.parent[at] = (g << L.ord_bits) | (u64)ord[j];
+            B.slot_of[at] = (u32)slot[j];
+            B.gidx_of[slot[j]] = (u32)at;
+          }
+        }
+      }
     }
-    if (err) atomicOr(&B.ctr->flags, (unsigned)LV_EVAL);
-    const bool stuck = live && !err && (fair == TLCG_FAIR_NONE || moves == 0);
+    err |= serr;
+    const bool stuck = live && !serr && (fair == TLCG_FAIR_NONE || moves == 0);
     if (live) B.stuck[g] = stuck;
-    const u64 e = wave_sum_u64((u64)edges), sk = wave_sum_u64((u64)stuck);
-    if (__lane_id() == 0) {
-      if (e) atomicAdd(&B.ctr->edges, (unsigned long long)e);
-      if (sk) atomicAdd(&B.ctr->stuck, (unsigned long long)sk);
-    }
+    nstuck += stuck;
+  }
+  if (err) atomicOr(&B.ctr->flags, (unsigned)LV_EVAL);
+  const u64 e = wave_sum_u64(edges), sk = wave_sum_u64(nstuck);
+  if (__lane_id() == 0) {
+    if (e) atomicAdd(&B.ctr->edges, (unsigned long long)e);
+    if (sk) atomicAdd(&B.ctr->stuck, (unsigned long long)sk);
   }
 }
 
@@ -248,7 +392,8 @@ __global__ __launch_bounds__(LV_BLOCK) void k_lv_zero(LvBufs<W> B, u64 n, u32* l
   for (u64 base = (u64)blockIdx.x * LV_BLOCK; base < n; base += stride) {
     const u64 g = base + threadIdx.x;
     const bool z = g < n && B.indeg[B.slot_of[g]] == 0;
-    const u64 at = wave_claim(z, &B.ctr->next);
+    u64 at = 0;
+    block_claim<1>(&z, &at, &B.ctr->next);
     if (z) list[at] = (u32)g;
   }
 }
@@ -264,22 +409,37 @@ __global__ __launch_bounds__(LV_BLOCK) void k_lv_peel(LvBufs<W> B, const u32* li
     const u64 i = base + threadIdx.x;
     const bool live = i < n;
     const W s = live ? B.store[list[i]] : (W)0;
-    for (int k = 0; k < kmax; ++k) {
-      W t = 0;
-      int ord = 0;
-      bool freed = false;
-      u32 tg = 0;
-      if (live && lv_move(L, s, k, &t, &ord) == 1 && !lv_p(L, t)) {
-        const u64 slot = lv_lookup<W>(B.slots, B.log2, t);
-        if (slot == ~0ull) {
-          atomicOr(&B.ctr->flags, (unsigned)LV_LOOKUP);
-        } else if (atomicSub(&B.indeg[slot], 1u) == 1u) {
-          freed = true;
-          tg = B.gidx_of[slot];
+    for (int k0 = 0; k0 < kmax; k0 += LV_BATCH) {
+      W t[LV_BATCH];
+      bool want[LV_BATCH];
+      u64 slot[LV_BATCH];
+#pragma unroll
+      for (int j = 0; j < LV_BATCH; ++j) {
+        t[j] = 0;
+        int ord = 0;
+        want[j] = live && k0 + j < kmax && lv_move(L, s, k0 + j, &t[j], &ord) == 1 && !lv_p(L, t[j]);
+      }
+      lv_lookup_batch(B, want, t, slot);
+      bool freed[LV_BATCH];
+      u32 tg[LV_BATCH];
+#pragma unroll
+      for (int j = 0; j < LV_BATCH; ++j) {
+        freed[j] = false;
+        tg[j] = 0;
+        if (want[j]) {
+          if (slot[j] == ~0ull) {
+            atomicOr(&B.ctr->flags, (unsigned)LV_LOOKUP);
+          } else if (atomicSub(&B.indeg[slot[j]], 1u) == 1u) {
+            freed[j] = true;
+            tg[j] = B.gidx_of[slot[j]];
+          }
         }
       }
-      const u64 at = wave_claim(freed, &B.ctr->next);
-      if (freed) next[at] = tg;
+      u64 ats[LV_BATCH];
+      block_claim<LV_BATCH>(freed, ats, &B.ctr->next);
+#pragma unroll
+      for (int j = 0; j < LV_BATCH; ++j)
+        if (freed[j]) next[ats[j]] = tg[j];
     }
   }
 }
@@ -291,7 +451,8 @@ __global__ __launch_bounds__(LV_BLOCK) void k_lv_left(LvBufs<W> B, u64 n, u32* l
   for (u64 base = (u64)blockIdx.x * LV_BLOCK; base < n; base += stride) {
     const u64 g = base + threadIdx.x;
     const bool z = g < n && B.indeg[B.slot_of[g]] != 0;
-    const u64 at = wave_claim(z, &B.ctr->next);
+    u64 at = 0;
+    block_claim<1>(&z, &at, &B.ctr->next);
     if (z) list[at] = (u32)g;
   }
 }
