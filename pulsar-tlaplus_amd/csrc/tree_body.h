@@ -21,25 +21,57 @@
 
 namespace tlcg {
 
-// CAP states per component, T FPSet slots (a power of 2, load <= CAP / T),
+// CAP states per component, T FPSet slots (a power of 2, load <= CAP / T;
+// closed mode scales its table to TLCG_TREE_TSCALE_CLOSED % of CAP instead),
 // G components per wavefront.  A component's depth holds ~16 states (P8) or
 // fewer, so one component per 64-lane wavefront leaves most lanes idle and
 // pays the scalar (exec-mask, loop) instructions once per state; G groups
 // share them.
+#ifndef TLCG_TREE_TSCALE_CLOSED
+#define TLCG_TREE_TSCALE_CLOSED 105
+#endif
 template <int CAP, int T, int G, bool CLOSED = false, typename W = u64>
 __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   constexpr int S = 64 / G;  // lanes per group
   static_assert((T & (T - 1)) == 0 && T >= CAP, "T: a power of 2 >= CAP");
-  __shared__ uint32_t h[G][T];       // key + 1, 0 = empty
-  __shared__ uint32_t keys[G][CAP];  // each component's keys in BFS (depth) order
-  __shared__ unsigned long long lvl_d[TREE_MAXLV], lvl_g[TREE_MAXLV];
+  // FPSet slots per component.  Closed mode: TLCG_TREE_TSCALE_CLOSED % of
+  // CAP (a multiple of 16, any size: multiply-shift slot hash), so a CU holds
+  // more wavefronts (G9-deep 42.1 -> 35.2 ms at 105 %: 672 slots, 12 instead
+  // of 9 workgroups per CU).  Producer mode keeps its power-of-2 T (a smaller
+  // table measured slower on P8: 2.34 vs 2.05 ms).  TLCG_TREE_TSCALE (A/B)
+  // scales both.
+#ifdef TLCG_TREE_TSCALE
+  constexpr int TT = (CAP * TLCG_TREE_TSCALE / 100 + 15) / 16 * 16;
+#else
+  constexpr int TT = CLOSED ? (CAP * TLCG_TREE_TSCALE_CLOSED / 100 + 15) / 16 * 16 : T;
+#endif
+  static_assert(TT >= CAP, "an FPSet holds a whole component");
+  constexpr bool TPOW2 = (TT & (TT - 1)) == 0;
+  __shared__ uint32_t h[G][TT];      // key + 1, 0 = empty
+#ifndef TLCG_TREE_KEYS_LDS
+  // A depth's states are read back from the group's HBM chunk (written
+  // before the __syncthreads that ends the insert step, so visible to the
+  // workgroup) and re-encoded, so the keys take no LDS and a CU holds more
+  // wavefronts: G9-deep 55.7 -> 42.1 ms, P8 2.74 -> 2.08 ms (same box;
+  // TLCG_TREE_KEYS_LDS = the keys in LDS, for A/B).
+  constexpr int KCAP = 1;
+#else
+  constexpr int KCAP = CAP;
+#endif
+  __shared__ uint32_t keys[G][KCAP];  // each component's keys in BFS (depth) order
+#ifdef TLCG_TREE_LVL32
+  typedef unsigned int lvl_t;  // a workgroup's per-depth sums fit 32 bits (it runs far fewer than 2^32 / CAP states)
+#else
+  typedef unsigned long long lvl_t;
+#endif
+  __shared__ lvl_t lvl_d[TREE_MAXLV], lvl_g[TREE_MAXLV];
   const int lane = threadIdx.x;
   const int g = lane / S, sub = lane % S;
   const u64 gmask = (S == 64 ? ~0ull : ((1ull << S) - 1)) << (g * S);  // my group's lanes
   const u64 below = lanemask_lt() & gmask;
   const int mb = L.msg_sh + L.N * L.mw;  // `messages` (with its length) occupies the low mb bits
   int log2t = 0;
-  while ((1 << log2t) < T) ++log2t;
+  while ((1 << log2t) < TT) ++log2t;
   for (int i = lane; i < TREE_MAXLV; i += 64) lvl_d[i] = lvl_g[i] = 0;
   __syncthreads();
   unsigned flags = 0;
@@ -66,15 +98,16 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   auto insert = [&](bool pred, uint32_t key, u64 pref, int dd) {
     bool isnew = false;
     if (pred) {
-      unsigned s = (key * 0x9E3779B1u) >> (32 - log2t);
-      for (int p = 0; p < T; ++p) {
+      unsigned s = TPOW2 ? (key * 0x9E3779B1u) >> (32 - log2t)
+                         : (unsigned)(((unsigned long long)(key * 0x9E3779B1u) * (unsigned)TT) >> 32);
+      for (int p = 0; p < TT; ++p) {
         const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
         if (old == 0) {
           isnew = true;
           break;
         }
         if (old == key + 1u) break;
-        s = (s + 1) & (T - 1);
+        s = TPOW2 ? (s + 1) & (TT - 1) : (s + 1 == (unsigned)TT ? 0u : s + 1);
       }
     }
     const u64 m = __ballot(isnew) & gmask;
@@ -83,7 +116,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       if (have) flags |= TREE_OVERFLOW;
     } else if (isnew) {
       const int pos = n + __popcll(m & below);
-      kk[pos] = key;
+      if (KCAP == CAP) kk[pos] = key;
       par[pos] = pref == NO_PARENT ? NO_PARENT : (a.rank_tag | pref);
       if constexpr (CLOSED) {
         st[pos] = code_word<W>(L, kc, msgs, key);
@@ -99,7 +132,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   while (true) {
     // a group without a component takes its next one
     if (!have && ci < a.n_comp) {
-      for (int i = sub * 4; i < T; i += S * 4) *reinterpret_cast<uint4*>(&hh[i]) = make_uint4(0, 0, 0, 0);
+      for (int i = sub * 4; i < TT; i += S * 4) *reinterpret_cast<uint4*>(&hh[i]) = make_uint4(0, 0, 0, 0);
       if constexpr (CLOSED) {
         np = 1;  // the component's initial state
         const W s0 = init_state<W>(L, a.comp0 + ci);
@@ -178,7 +211,14 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     for (int b = f0; __ballot(have && b < f1); b += S) {
       const int i = b + sub;
       const bool ok = have && i < f1;
-      const uint32_t k = ok ? kk[i] : 0;
+      uint32_t k = 0;
+      if constexpr (CLOSED && KCAP != CAP) {
+        if (ok) k = code_encode_w<W>(L, st[i]);
+      } else if constexpr (KCAP != CAP) {
+        if (ok) k = (uint32_t)((u64)st[i] >> mb);
+      } else {
+        k = ok ? kk[i] : 0;
+      }
       uint32_t t = 0, t2 = 0;
       int act = 0, r, nsucc;
       bool crash;
@@ -203,8 +243,8 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
 #pragma unroll
     for (int off = S / 2; off > 0; off >>= 1) gen += __shfl_xor(gen, off);
     if (have && sub == 0 && d < TREE_MAXLV) {
-      atomicAdd(&lvl_d[d], (unsigned long long)(f1 - f0));
-      atomicAdd(&lvl_g[d], gen);
+      atomicAdd(&lvl_d[d], (lvl_t)(f1 - f0));
+      atomicAdd(&lvl_g[d], (lvl_t)gen);
     }
     __syncthreads();
     if (have) {
@@ -224,8 +264,8 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   }
   __syncthreads();
   for (int i = lane; i < TREE_MAXLV; i += 64) {
-    if (lvl_d[i]) atomicAdd(&a.lvl[i], lvl_d[i]);
-    if (lvl_g[i]) atomicAdd(&a.lvl_gen[i], lvl_g[i]);
+    if (lvl_d[i]) atomicAdd(&a.lvl[i], (unsigned long long)lvl_d[i]);
+    if (lvl_g[i]) atomicAdd(&a.lvl_gen[i], (unsigned long long)lvl_g[i]);
   }
 }
 
