@@ -110,8 +110,14 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
     return false;
   }
   const std::string a = "--offload-arch=" + arch;
-  const char* opts[] = {a.c_str(), "-O3", "-std=c++20"};
-  const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+  std::vector<std::string> extra;  // tuning experiments: TLCG_JIT_OPTS="-mllvm -x=1 ..." (part of the cache key)
+  if (const char* e = std::getenv("TLCG_JIT_OPTS")) {
+    std::istringstream in(e);
+    for (std::string w; in >> w;) extra.push_back(w);
+  }
+  std::vector<const char*> opts = {a.c_str(), "-O3", "-std=c++20"};
+  for (const std::string& w : extra) opts.push_back(w.c_str());
+  const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   if (r != HIPRTC_SUCCESS) {
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
@@ -143,7 +149,8 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
   arch = arch.substr(0, arch.find(':'));
   const std::string src = program_source(L);
   char key[64];
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2"));
+  const char* jo = std::getenv("TLCG_JIT_OPTS");
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2" + (jo ? jo : "")));
   const std::string dir = cache_dir();
   const std::string path = dir + "/" + key + "-" + arch + ".co";
   std::vector<char> code;
