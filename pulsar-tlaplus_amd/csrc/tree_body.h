@@ -28,7 +28,7 @@ namespace tlcg {
 // pays the scalar (exec-mask, loop) instructions once per state; G groups
 // share them.
 #ifndef TLCG_TREE_TSCALE_CLOSED
-#define TLCG_TREE_TSCALE_CLOSED 105
+#define TLCG_TREE_TSCALE_CLOSED 100
 #endif
 template <int CAP, int T, int G, bool CLOSED = false, typename W = u64>
 __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
@@ -37,7 +37,8 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   // FPSet slots per component.  Closed mode: TLCG_TREE_TSCALE_CLOSED % of
   // CAP (a multiple of 16, any size: multiply-shift slot hash), so a CU holds
   // more wavefronts (G9-deep 42.1 -> 35.2 ms at 105 %: 672 slots, 12 instead
-  // of 9 workgroups per CU).  Producer mode keeps its power-of-2 T (a smaller
+  // of 9 workgroups per CU; with the frontier buffer below, 100 % = 640
+  // slots measured 31.2 vs 33.6 ms).  Producer mode keeps its power-of-2 T (a smaller
   // table measured slower on P8: 2.34 vs 2.05 ms).  TLCG_TREE_TSCALE (A/B)
   // scales both.
 #ifdef TLCG_TREE_TSCALE
@@ -59,6 +60,22 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   constexpr int KCAP = CAP;
 #endif
   __shared__ uint32_t keys[G][KCAP];  // each component's keys in BFS (depth) order
+  // FB: the first FB keys of the depth being expanded and of the next one
+  // stay in LDS (two buffers by depth parity), so the expansion reads the
+  // store only past them -- no HBM load (behind the previous depth's stores)
+  // and no re-encode on the common path.  0 = off.  Closed mode: 16 (G9-deep
+  // 35.2 -> 31.2 ms with 640-slot tables, profiles/r02_tree_fb_ab.jsonl; a
+  // depth of G9-deep holds 7.5 states on average); Producer mode: off (P8
+  // 2.06 vs 2.09 / 2.20 ms at 32 / 16).
+#ifndef TLCG_TREE_FB
+#define TLCG_TREE_FB 16
+#endif
+#ifndef TLCG_TREE_FB_OPEN
+#define TLCG_TREE_FB_OPEN 0
+#endif
+  constexpr int FB = KCAP == CAP ? 0 : CLOSED ? TLCG_TREE_FB : TLCG_TREE_FB_OPEN;
+  __shared__ uint32_t fbuf[G][2][FB > 0 ? FB : 1];
+  int dbase = 0;  // the first position of the depth being inserted (FB)
 #ifdef TLCG_TREE_LVL32
   typedef unsigned int lvl_t;  // a workgroup's per-depth sums fit 32 bits (it runs far fewer than 2^32 / CAP states)
 #else
@@ -109,6 +126,13 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         if (old == key + 1u) break;
         s = TPOW2 ? (s + 1) & (TT - 1) : (s + 1 == (unsigned)TT ? 0u : s + 1);
       }
+      // a table of exactly CAP slots is full once the chunk is: a state it
+      // could not take would be lost, so a full chunk sends the component on
+      // (a component of exactly CAP states too, conservatively); a larger
+      // table always has a free slot while the chunk has room
+      if constexpr (TT == CAP) {
+        if (n >= CAP) flags |= TREE_OVERFLOW;
+      }
     }
     const u64 m = __ballot(isnew) & gmask;
     const int cnt = __popcll(m);
@@ -117,6 +141,9 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     } else if (isnew) {
       const int pos = n + __popcll(m & below);
       if (KCAP == CAP) kk[pos] = key;
+      if constexpr (FB > 0) {
+        if (pos - dbase < FB) fbuf[g][dd & 1][pos - dbase] = key;
+      }
       par[pos] = pref == NO_PARENT ? NO_PARENT : (a.rank_tag | pref);
       if constexpr (CLOSED) {
         st[pos] = code_word<W>(L, kc, msgs, key);
@@ -183,6 +210,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     if (have && d >= TREE_MAXLV - 1) flags |= TREE_OVERFLOW;
     // the entries at depth d (parents at depth d - 1; pdep is nondecreasing)
     bool more = have && e < np;
+    dbase = f0;  // entries join depth d, which starts at f0
     while (__ballot(more)) {
       const u64 i = e + (u64)sub;
       bool ok = more && i < np;
@@ -208,11 +236,18 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     const int f1 = n;  // depth d = [f0, f1)
     // expand depth d: compactor and BrokerCrash successors at depth d + 1
     u64 gen = 0;
+    dbase = f1;  // depth d + 1 starts at f1
     for (int b = f0; __ballot(have && b < f1); b += S) {
       const int i = b + sub;
       const bool ok = have && i < f1;
       uint32_t k = 0;
-      if constexpr (CLOSED && KCAP != CAP) {
+      if constexpr (FB > 0) {
+        if (ok && i - f0 < FB) k = fbuf[g][d & 1][i - f0];
+        else if (ok) {
+          if constexpr (CLOSED) k = code_encode_w<W>(L, st[i]);
+          else k = (uint32_t)((u64)st[i] >> mb);
+        }
+      } else if constexpr (CLOSED && KCAP != CAP) {
         if (ok) k = code_encode_w<W>(L, st[i]);
       } else if constexpr (KCAP != CAP) {
         if (ok) k = (uint32_t)((u64)st[i] >> mb);
