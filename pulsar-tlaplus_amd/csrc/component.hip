@@ -28,7 +28,7 @@ void launch_k(const CompArgs& a, int K, bool code, unsigned grid, hipStream_t st
 bool launch_component(const CompArgs& a, int K, bool code, hipStream_t stream) {
   if (!a.n_comp) return true;
   const u64 batches = (a.n_comp + 63) / 64;
-  const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
+  const unsigned grid = (unsigned)(batches < comp_grid_cap() ? batches : comp_grid_cap());
   if (a.outdeg) launch_k<true>(a, K, code && K <= 64, grid, stream);
   else launch_k<false>(a, K, code && K <= 64, grid, stream);
   return hipGetLastError() == hipSuccess;

@@ -66,6 +66,15 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 #define TLCG_CODE_FPSET_NUM 5
 #define TLCG_CODE_FPSET_DEN 4
 #endif
+// the queue and the FPSet in lane columns (A/B only: measured slower, G9
+// 6.18 vs 5.80 ms, M8 1.251 vs 1.224, with the same SQ_LDS_BANK_CONFLICT
+// count -- the conflicts are the 64 lanes' same-address per-level adds, 60
+// extra cycles x 20 levels x batches exactly, not the probes: the lanes of
+// a wave run isomorphic components in lockstep, so their probes hit one
+// slot row; profiles/r03_pmc_component_g9.json)
+#ifndef TLCG_LDS_COLS
+#define TLCG_LDS_COLS 0
+#endif
 #ifndef TLCG_CODE_MAXLV
 #define TLCG_CODE_MAXLV 32
 #endif
@@ -84,9 +93,36 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
   constexpr int T = CODE ? CodeShape<K>::T : CompShape<K>::T;
   constexpr int LV = CODE && TLCG_CODE_MAXLV < COMP_MAXLV ? TLCG_CODE_MAXLV : COMP_MAXLV;  // levels tracked
   typedef typename tsel<CODE, uint16_t, uint32_t>::type qword;
+  const int lane = threadIdx.x;
+#if TLCG_LDS_COLS
+  // lane columns: every dword of the queue and of the FPSet belongs to one
+  // lane (dword [r][l]), so the sub-dword reads and writes of a wave hit bank
+  // l mod 32 whatever slots or positions its lanes touch.  (Rows of 64 bytes
+  // put four lanes' slots in one dword: two lanes of a quad at different
+  // slots of one bank parity collided, 51 % of the LDS-array cycles of G9
+  // were conflicts, profiles/r02_pmc_component.json.)
+  constexpr int QPD = 4 / (int)sizeof(qword);     // queue entries per dword
+  __shared__ uint32_t qcol[(K + QPD - 1) / QPD][64];
+  qword* const ql = reinterpret_cast<qword*>(&qcol[0][lane]);
+  // queue entry p of this lane: entry p % QPD of dword [p / QPD][lane]
+  auto Q = [&](unsigned p) -> qword& {
+    return QPD == 1 ? ql[p << 6] : ql[((p & ~(unsigned)(QPD - 1)) << 6) | (p & (unsigned)(QPD - 1))];
+  };
+#else
   __shared__ qword q[K][64];                      // FIFO of local keys (word >> msgs_bits) or codes
+  auto Q = [&](unsigned p) -> qword& { return q[p][lane]; };
+#endif
 #ifndef TLCG_BUCKETS  // linear probing over byte slots (the bucketized table measured no faster)
+#if TLCG_LDS_COLS
+  static_assert(T % 4 == 0, "FPSet slots in whole dwords");
+  __shared__ uint32_t hcol[T / 4][64];            // FPSet: slot s of lane l = byte s % 4 of dword [s / 4][l]
+  uint8_t(*const h)[64] = reinterpret_cast<uint8_t(*)[64]>(&hcol[0][0]);  // (the whole table, for clearing)
+  uint8_t* const hl = reinterpret_cast<uint8_t*>(&hcol[0][lane]);
+  auto H = [&](unsigned s) -> uint8_t& { return hl[((s & ~3u) << 6) | (s & 3u)]; };  // 1 + queue position, 0 = empty
+#else
   __shared__ uint8_t h[T][64];                    // FPSet: 1 + queue position, 0 = empty
+  auto H = [&](unsigned s) -> uint8_t& { return h[s][lane]; };
+#endif
 #else
   // FPSet: T / 4 buckets of four 1-byte slots (1 + queue position, 0 = empty);
   // bucket b of lane l is the dword hb[b][l], so a wave's bucket reads hit 64
@@ -99,7 +135,6 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
   // per level: distinct states (low 32 bits) + successors generated by
   // expanding the level (high 32 bits), one packed 64-bit LDS add per lane and level
   __shared__ unsigned long long lvl_sh[LV];
-  const int lane = threadIdx.x;
   const int mb = L.msg_sh + L.N * L.mw;  // `messages` occupies the low mb bits
   if (lane < LV) lvl_sh[lane] = 0;
   u64 gen = 0, dist = 0;
@@ -148,11 +183,11 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     }
     if (act && alive) {
 #ifndef TLCG_BUCKETS
-      h[slot_of<T>(k0)][lane] = 1;
+      H(slot_of<T>(k0)) = 1;
 #else
       hb[bucket_of<NB>(k0)][lane] = 1;
 #endif
-      q[0][lane] = k0;
+      Q(0) = k0;
       tail = 1;
       st[0] = s0;
       par[0] = NO_PARENT;
@@ -170,7 +205,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     // the insert of a new state: queue, HBM store + parent log; returns the
     // first failing invariant + 1 (0: all hold)
     auto insert = [&](lkey key, int action, int pos) -> int {
-      q[tail][lane] = (qword)key;
+      Q(tail) = (qword)key;
 #ifndef TLCG_NO_STORE  // (experiment only: measures what the HBM store costs)
       const unsigned off = (unsigned)(tail * 64 + lane) * 8u;
       lkey lk = key;
@@ -197,26 +232,26 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       // slot, or the state itself), so the divergent loop's exec-mask
       // bookkeeping is paid only on a collision
       if (e != 0) {
-        if (q[e - 1][lane] == key) return Visit{-1, 0};  // seen
+        if (Q(e - 1) == key) return Visit{-1, 0};  // seen
         for (int p = 1; p < T; ++p) {
           sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
-          e = h[sl][lane];
+          e = H(sl);
           if (e == 0) break;
-          if (q[e - 1][lane] == key) return Visit{-1, 0};  // seen
+          if (Q(e - 1) == key) return Visit{-1, 0};  // seen
         }
       }
 #else
       for (int p = 0; p < T; ++p) {
         if (e == 0) break;
-        if (q[e - 1][lane] == key) return Visit{-1, 0};  // seen
+        if (Q(e - 1) == key) return Visit{-1, 0};  // seen
         sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
-        e = h[sl][lane];
+        e = H(sl);
       }
 #endif
 #if !TLCG_COMP_FLAT
       if (tail >= K) return Visit{-2, 0};  // does not fit on chip: cascade
 #endif
-      h[sl][lane] = (uint8_t)(tail + 1);
+      H(sl) = (uint8_t)(tail + 1);
       return Visit{(int)sl | (insert(key, action, pos) << 16), 0};
     };
 #else
@@ -230,8 +265,8 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     auto visit = [&](lkey key, int action, int pos, unsigned b, uint32_t w) -> Visit {
       for (int step = 0; step < NB; ++step) {
         const unsigned e0 = w & 255u, e1 = (w >> 8) & 255u, e2 = (w >> 16) & 255u, e3 = w >> 24;
-        const lkey q0 = q[e0 ? e0 - 1 : 0][lane], q1 = q[e1 ? e1 - 1 : 0][lane];
-        const lkey q2 = q[e2 ? e2 - 1 : 0][lane], q3 = q[e3 ? e3 - 1 : 0][lane];
+        const lkey q0 = Q(e0 ? e0 - 1 : 0), q1 = Q(e1 ? e1 - 1 : 0);
+        const lkey q2 = Q(e2 ? e2 - 1 : 0), q3 = Q(e3 ? e3 - 1 : 0);
         if ((e0 && q0 == key) | (e1 && q1 == key) | (e2 && q2 == key) | (e3 && q3 == key)) return Visit{-1, 0};
         const uint32_t z = (w - 0x01010101u) & ~w & 0x80808080u;  // lowest set bit: the first empty slot
         if (z) {
@@ -278,7 +313,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       const lkey s = cur;
       const int tail0 = tail;
       // (read unconditionally, clamped into the queue: no masked LDS read)
-      const lkey nxt = q[head + 1 < K ? head + 1 : K - 1][lane];
+      const lkey nxt = Q(head + 1 < K ? head + 1 : K - 1);
       int nsucc = 0;
       lkey t = 0;
       int action = 0;
@@ -314,8 +349,8 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       // both successors' first FPSet slots (buckets) are read together
 #ifndef TLCG_BUCKETS
       const unsigned sl1 = slot_of<T>(t), sl2 = slot_of<T>(t2);
-      const unsigned e1 = h[sl1][lane];  // (unconditional reads; unused when the action is disabled)
-      unsigned e2 = h[sl2][lane];
+      const unsigned e1 = H(sl1);  // (unconditional reads; unused when the action is disabled)
+      unsigned e2 = H(sl2);
 #else
       const unsigned sl1 = bucket_of<NB>(t), sl2 = bucket_of<NB>(t2);
       const uint32_t e1 = r == 1 ? hb[sl1][lane] : 0u;
@@ -330,7 +365,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
         if (ins >= 0) first_new = t;
         ev1 = v1.code >= 0 ? v1.code >> 16 : 0;
 #ifndef TLCG_BUCKETS
-        if (ins == (int)sl2 && crash) e2 = h[sl2][lane];  // the slot just taken
+        if (ins == (int)sl2 && crash) e2 = H(sl2);  // the slot just taken
 #else
         if (ins == (int)sl2) e2 = v1.nw;  // the bucket just written
 #endif
@@ -438,19 +473,20 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) ev = min(ev, (unsigned long long)__shfl_xor(ev, off));
   __syncthreads();
+  const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy
   if (lane == 0) {
-    if (gen) atomicAdd(&a.totals[0], (unsigned long long)gen);
-    if (dist) atomicAdd(&a.totals[1], (unsigned long long)dist);
+    if (gen) atomicAdd(&a.totals[so + 0], (unsigned long long)gen);
+    if (dist) atomicAdd(&a.totals[so + 1], (unsigned long long)dist);
     if (ev != NO_EVENT) atomicMin(a.event, ev);
     if constexpr (OD) {
-      if (o0) atomicAdd(&a.outdeg[0], (unsigned long long)o0);
-      if (o1) atomicAdd(&a.outdeg[1], (unsigned long long)o1);
-      if (o2) atomicAdd(&a.outdeg[2], (unsigned long long)o2);
+      if (o0) atomicAdd(&a.outdeg[so + 0], (unsigned long long)o0);
+      if (o1) atomicAdd(&a.outdeg[so + 1], (unsigned long long)o1);
+      if (o2) atomicAdd(&a.outdeg[so + 2], (unsigned long long)o2);
     }
   }
   if (lane < LV && lvl_sh[lane]) {
-    atomicAdd(&a.lvl[lane], lvl_sh[lane] & 0xffffffffull);
-    if (lvl_sh[lane] >> 32) atomicAdd(&a.lvl_gen[lane], lvl_sh[lane] >> 32);
+    atomicAdd(&a.lvl[so + lane], lvl_sh[lane] & 0xffffffffull);
+    if (lvl_sh[lane] >> 32) atomicAdd(&a.lvl_gen[so + lane], lvl_sh[lane] >> 32);
   }
 }
 

@@ -208,7 +208,7 @@ bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool co
   hipFunction_t f = a.outdeg ? k.component_od[i] : k.component[i];
   if (code && i < 2) f = a.outdeg ? k.code_od[i] : k.code[i];
   const uint64_t batches = (a.n_comp + 63) / 64;
-  const unsigned grid = (unsigned)(batches < 65536 ? batches : 65536);
+  const unsigned grid = (unsigned)(batches < comp_grid_cap() ? batches : comp_grid_cap());
   CompArgs copy = a;
   void* args[] = {&copy};
   return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;

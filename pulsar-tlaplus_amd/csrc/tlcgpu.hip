@@ -1748,7 +1748,7 @@ bool component_applicable(const tlcg_ctx* c) {
 
 bool comp_scratch(tlcg_ctx* c, u64 n) {
   if (!c->d_comp) {
-    const size_t bytes = sizeof(unsigned long long) * kCompCounters;
+    const size_t bytes = sizeof(unsigned long long) * kCompCounters * COMP_STRIPES;
     if (!alloc_bytes(c, (void**)&c->d_comp, bytes, "component counters")) return false;
     HIPCHK(hipHostMalloc((void**)&c->h_comp, bytes));
   }
@@ -1815,7 +1815,7 @@ int run_component(tlcg_ctx* c) {
       HIPCHK_I(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
     }
     const int out = cur == 0 ? 1 : 0;
-    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * kCompCounters, c->stream));
+    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * kCompCounters * COMP_STRIPES, c->stream));
     HIPCHK_I(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
     CompArgs a;
     a.L = L;
@@ -1834,6 +1834,8 @@ int run_component(tlcg_ctx* c) {
     a.outdeg = c->opts.outdegree ? c->d_comp + COMP_MAXLV + 4 : nullptr;
     a.lvl_gen = c->d_comp + COMP_MAXLV + 7;
     a.ovf_list = c->d_ovf[out];
+    a.stripe = kCompCounters;
+    a.nstripe = COMP_STRIPES;
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
     // the first pass runs component codes when they fit 16 bits (component_code.h);
     // a component whose initial key is no code, and the cascade, run 32-bit keys
@@ -1843,9 +1845,15 @@ int run_component(tlcg_ctx* c) {
       return -1;
     }
     HIPCHK_I(hipEventRecord(c->e1, c->stream));
-    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * kCompCounters,
+    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * kCompCounters * COMP_STRIPES,
                           hipMemcpyDeviceToHost, c->stream));
     HIPCHK_I(hipStreamSynchronize(c->stream));
+    // fold the stripes into copy 0 (the event and the overflow count live there only)
+    for (int sidx = 1; sidx < COMP_STRIPES; ++sidx) {
+      const unsigned long long* h = c->h_comp + (size_t)sidx * kCompCounters;
+      for (int i = 0; i < kCompCounters; ++i)
+        if (i != COMP_MAXLV + 2 && i != COMP_MAXLV + 3) c->h_comp[i] += h[i];
+    }
     float ms = 0;
     hipEventElapsedTime(&ms, c->e0, c->e1);
     c->kernel_ms += ms;
@@ -1938,7 +1946,7 @@ int run_tree(tlcg_ctx* c) {
   u64 comps = 0;
   for (u64 x : ncomp) comps += x;
   if (!c->d_tree_ctr) {
-    const size_t bytes = sizeof(unsigned long long) * (2 * TREE_MAXLV + 2);
+    const size_t bytes = sizeof(unsigned long long) * (2 * TREE_MAXLV * TREE_STRIPES + 2);
     if (!alloc_bytes(c, (void**)&c->d_tree_ctr, bytes, "tree counters")) return -1;
     HIPCHK_I(hipHostMalloc((void**)&c->h_tree_ctr, bytes));
   }
@@ -1983,7 +1991,8 @@ int run_tree(tlcg_ctx* c) {
       c->tree_comps = comps;
     }
     unsigned long long* ctr = c->d_tree_ctr;
-    HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * (2 * TREE_MAXLV + 2), c->stream));
+    constexpr int kTreeCtr = 2 * TREE_MAXLV * TREE_STRIPES + 2;  // [stripe][lvl, lvl_gen], flags, max_n
+    HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * kTreeCtr, c->stream));
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
     u64 gbase = 0, cbase = 0, pgbase = 0, pcbase = 0;
     for (size_t l = 0; l < ncomp.size(); ++l) {
@@ -2005,8 +2014,10 @@ int run_tree(tlcg_ctx* c) {
       a.rank_tag = (u64)c->opts.rank << 56;
       a.lvl = ctr;
       a.lvl_gen = ctr + TREE_MAXLV;
-      a.flags = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV);
-      a.max_n = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV + 1);
+      a.flags = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV * TREE_STRIPES);
+      a.max_n = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV * TREE_STRIPES + 1);
+      a.stripe = 2 * TREE_MAXLV;
+      a.nstripe = TREE_STRIPES;
       const bool jit = c->jit_used && (cap == 384 || cap == 1024 || cap == 640 || cap == 2048);
       const int g = cap == 384 || cap == 640 ? groups : 1;
       if (!(jit ? jit_launch_tree(c->jit, a, cap, c->stream) : launch_tree(a, cap, g, closed, words, c->stream))) {
@@ -2019,14 +2030,16 @@ int run_tree(tlcg_ctx* c) {
       cbase += a.n_comp;
     }
     HIPCHK_I(hipEventRecord(c->e1, c->stream));
-    HIPCHK_I(hipMemcpyAsync(c->h_tree_ctr, ctr, sizeof(unsigned long long) * (2 * TREE_MAXLV + 2),
-                            hipMemcpyDeviceToHost, c->stream));
+    HIPCHK_I(hipMemcpyAsync(c->h_tree_ctr, ctr, sizeof(unsigned long long) * kTreeCtr, hipMemcpyDeviceToHost,
+                            c->stream));
     HIPCHK_I(hipStreamSynchronize(c->stream));
+    for (int sidx = 1; sidx < TREE_STRIPES; ++sidx)  // fold the stripes into copy 0
+      for (int i = 0; i < 2 * TREE_MAXLV; ++i) c->h_tree_ctr[i] += c->h_tree_ctr[(size_t)sidx * 2 * TREE_MAXLV + i];
     float ms = 0;
     hipEventElapsedTime(&ms, c->e0, c->e1);
     c->kernel_ms += ms;
     c->expand_ms += ms;
-    const unsigned flags = (unsigned)c->h_tree_ctr[2 * TREE_MAXLV];
+    const unsigned flags = (unsigned)c->h_tree_ctr[2 * TREE_MAXLV * TREE_STRIPES];
     if (flags & TREE_EVENT) return 0;  // the global engine finds TLC's first error and its trace
     if (flags & TREE_OVERFLOW) continue;
     c->tree_cap = cap;

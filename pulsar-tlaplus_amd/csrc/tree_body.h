@@ -134,16 +134,19 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         }
         s = TPOW2 ? (s + 1) & (TT - 1) : (s + 1 == (unsigned)TT ? 0u : s + 1);
       }
-      // a table of exactly CAP slots is full once the chunk is: a state it
-      // could not take would be lost, so a full chunk sends the component on
-      // (a component of exactly CAP states too, conservatively); a larger
-      // table always has a free slot while the chunk has room
-      if constexpr (TT == CAP) {
-        if (n >= CAP) flags |= TREE_OVERFLOW;
-      }
     }
     const u64 m = __ballot(isnew) & gmask;
     const int cnt = __popcll(m);
+    // a table of exactly CAP slots is full once the chunk is, and a lane
+    // whose probe found neither its key nor an empty slot lost its state: a
+    // chunk filled by this insert (or already full) sends the component on --
+    // a component of exactly CAP states too, conservatively (the
+    // check before the ballot missed the lanes that lost the last free slot
+    // to another lane of the same insert); a larger table always has a free
+    // slot while the chunk has room
+    if constexpr (TT == CAP) {
+      if (have && n + cnt >= CAP) flags |= TREE_OVERFLOW;
+    }
     if (n + cnt > CAP) {
       if (have) flags |= TREE_OVERFLOW;
     } else if (isnew) {
@@ -306,9 +309,10 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     atomicMax(a.max_n, maxn);
   }
   __syncthreads();
+  const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy
   for (int i = lane; i < TREE_MAXLV; i += 64) {
-    if (lvl_d[i]) atomicAdd(&a.lvl[i], (unsigned long long)lvl_d[i]);
-    if (lvl_g[i]) atomicAdd(&a.lvl_gen[i], (unsigned long long)lvl_g[i]);
+    if (lvl_d[i]) atomicAdd(&a.lvl[so + i], (unsigned long long)lvl_d[i]);
+    if (lvl_g[i]) atomicAdd(&a.lvl_gen[so + i], (unsigned long long)lvl_g[i]);
   }
 }
 
