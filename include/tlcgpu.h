@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TLCG_ABI_VERSION 2
+#define TLCG_ABI_VERSION 3
 #define TLCG_MAX_SET 63 /* largest KeySpace / ValueSpace */
 #define TLCG_MAX_INV 8
 
@@ -46,7 +46,10 @@ enum {
   TLCG_INV_TYPESAFE = 0,            /* TypeSafe */
   TLCG_INV_COMPACTED_LEDGER_LEAK = 1, /* CompactedLedgerLeak */
   TLCG_INV_HORIZON_CORRECTNESS = 2, /* CompactionHorizonCorrectness */
-  TLCG_INV_DUP_NULLKEY_MESSAGE = 3  /* DuplicateNullKeyMessage */
+  TLCG_INV_DUP_NULLKEY_MESSAGE = 3, /* DuplicateNullKeyMessage */
+  /* TLCG_INV_USER + j: the j-th definition of tlcg_model.user_defs (an
+   * invariant the user added to the module: BASELINE config 5) */
+  TLCG_INV_USER = 16
 };
 
 /* Next disjuncts, source order (compaction.tla:216-231); -1 = Init */
@@ -90,6 +93,18 @@ typedef struct tlcg_model {
   int64_t values[TLCG_MAX_SET];    /* ValueSpace elements */
   int32_t n_invariants;
   int32_t invariants[TLCG_MAX_INV]; /* TLCG_INV_* in cfg order */
+  /* Definitions user invariants may use (NULL: none), as TLA+ text: each
+   * definition is a header line "@@DEF <name> [<param> ...] [@<line>]"
+   * followed by its body as written in the module (columns kept: bulleted
+   * /\ and \/ lists are read by column).  TLCG_INV_USER + j names the j-th
+   * definition.  A user invariant is a state predicate over the spec's
+   * variables and constants (the subset user_inv.cpp documents); one outside
+   * it is refused at tlcg_create / tlcg_check_model, never checked
+   * approximately.  Models with user invariants run on the global engine,
+   * one rank.  The text is copied by tlcg_create.  (ModelChecker's
+   * invariant list, compaction.cfg:25-31, with invariants the user defined
+   * in the .tla, compaction.tla:236-294 being the spec's own.) */
+  const char* user_defs;
 } tlcg_model;
 
 typedef struct tlcg_opts {
@@ -238,6 +253,9 @@ int tlcg_host_init_state_words(const tlcg_model* m, uint64_t idx, uint64_t* out)
 int tlcg_host_successors_words(const tlcg_model* m, const uint64_t* state, uint64_t* out, int32_t* actions,
                                int32_t cap);
 int tlcg_host_check_invariants_words(const tlcg_model* m, const uint64_t* state);
+/* The same for n states (tlcg_state_words words each) into out[i]: one model
+ * build (and user-invariant compile) for the batch.  0, or -2 on a bad model. */
+int tlcg_host_check_invariants_batch(const tlcg_model* m, const uint64_t* states, uint64_t n, int32_t* out);
 /* Self-check of the component engine's specialized evaluators against the
  * generic ones on the components of initial states [first, first + n), host
  * only.  Returns the states compared (0: the component engine does not take

@@ -32,12 +32,18 @@ class EvalError(Exception):
 class Model:
     def __init__(self, N=3, C=3, K=1, keys=(1, 2), values=(1, 2), retain=True,
                  producer=False, consumer=False, ctl=2,
-                 invariants=("TypeSafe", "CompactionHorizonCorrectness"), deadlock=True):
+                 invariants=("TypeSafe", "CompactionHorizonCorrectness"), deadlock=True, user_defs=None):
         self.N, self.C, self.K, self.ctl = N, C, K, ctl
         self.keyset = sorted(set(keys) | {0})      # KeySet, compaction.tla:49
         self.valueset = sorted(set(values) | {0})  # ValueSet, compaction.tla:50
         self.retain, self.producer, self.consumer = retain, producer, consumer
         self.invariants, self.deadlock = tuple(invariants), deadlock
+        # invariants the user added to the module (BASELINE config 5): their own
+        # parser/evaluator, oracle/tla_eval.py (test infrastructure)
+        self.user = None
+        if user_defs:
+            from tla_eval import Evaluator
+            self.user = Evaluator(self, user_defs)
 
     # state = (messages, ledgers, cursor, phase, p1r, horizon, context, crash, consume)
     def inits(self):
@@ -131,6 +137,12 @@ class Model:
         return led[ctx - 1]
 
     def inv(self, name, s):
+        if self.user is not None and name in self.user.defs:
+            import tla_eval
+            try:
+                return self.user.holds(name, s)
+            except tla_eval.EvalError as e:
+                raise EvalError(str(e))
         msgs, led, cur, ph, p1r, hz, ctx, crash, cons = s
         N, C = self.N, self.C
         if name == "TypeSafe":  # :236-248

@@ -40,8 +40,12 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
     if (v == 0) return fail("Assumption 0 \\notin ValueSpace is false.");
   }
   if (m.n_invariants < 0 || m.n_invariants > TLCG_MAX_INV) return fail("too many invariants");
-  for (int q = 0; q < m.n_invariants; ++q)
-    if (m.invariants[q] < 0 || m.invariants[q] >= N_INVARIANT_KINDS) return fail("unknown invariant id");
+  const std::vector<std::string> udefs = user_def_names(m.user_defs);
+  for (int q = 0; q < m.n_invariants; ++q) {
+    const int kind = m.invariants[q];
+    const bool user = kind >= TLCG_INV_USER && kind - TLCG_INV_USER < (int)udefs.size();
+    if (!user && (kind < 0 || kind >= N_INVARIANT_KINDS)) return fail("unknown invariant id");
+  }
   HostModel hm;
   ks.push_back(0);
   vs.push_back(0);
@@ -110,6 +114,24 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
     hm.n_init = c;
   }
   hm.max_new_per_state = (L.producer ? L.nkv : 0) + 2;
+  // user invariants (user_inv.h): the distinct definitions the cfg names, in
+  // first-use order, become program entries 0, 1, ..; L.inv holds INV_USER + entry
+  std::vector<std::string> names;
+  for (int q = 0; q < m.n_invariants; ++q) {
+    if (m.invariants[q] < TLCG_INV_USER) continue;
+    const std::string& nm = udefs[(size_t)(m.invariants[q] - TLCG_INV_USER)];
+    size_t k = std::find(names.begin(), names.end(), nm) - names.begin();
+    if (k == names.size()) names.push_back(nm);
+    L.inv[q] = INV_USER + (int)k;
+  }
+  if (!names.empty()) {
+    auto prog = std::make_shared<UserProg>();
+    std::string e;
+    if (!compile_user_invariants(m, hm, names, prog.get(), &e)) return fail(e);
+    hm.user = prog;
+    hm.user_defs = m.user_defs;
+    L.defer_inv = 1;
+  }
   *out = hm;
   return true;
 }
@@ -365,14 +387,23 @@ int tlcg_host_check_invariants_words(const tlcg_model* m, const uint64_t* state)
   HostModel hm;
   std::string e;
   if (!m || !state || !build_model(*m, &hm, &e)) return -2;
-  return check_invariants<u128>(hm.L, join_words(state, state_words(hm.L)));
+  return host_check_all<u128>(hm, join_words(state, state_words(hm.L)));
+}
+
+int tlcg_host_check_invariants_batch(const tlcg_model* m, const uint64_t* states, uint64_t n, int32_t* out) {
+  HostModel hm;
+  std::string e;
+  if (!m || !states || !out || !build_model(*m, &hm, &e)) return -2;
+  const int w = state_words(hm.L);
+  for (uint64_t i = 0; i < n; ++i) out[i] = host_check_all<u128>(hm, join_words(states + i * (uint64_t)w, w));
+  return 0;
 }
 
 int tlcg_host_check_invariants(const tlcg_model* m, uint64_t state) {
   HostModel hm;
   std::string e;
   if (!m || !build_model(*m, &hm, &e) || state_words(hm.L) != 1) return -2;
-  return check_invariants(hm.L, state);
+  return host_check_all(hm, state);
 }
 
 // PROPERTY Termination == <>(Len(messages) = MessageSentLimit /\
@@ -404,6 +435,7 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
   HostModel hm;
   std::string e;
   if (!m || !build_model(*m, &hm, &e) || hm.L.producer) return -1;
+  if (hm.user) return 0;  // user invariants run on the global engine only
   const Layout& L = hm.L;
   int64_t checked = 0;
   const int mb = L.led_sh;

@@ -4,8 +4,11 @@
 #include <string>
 #include <vector>
 
+#include <memory>
+
 #include "model.h"
 #include "tlcgpu.h"
+#include "user_inv.h"
 
 namespace tlcg {
 
@@ -15,7 +18,21 @@ struct HostModel {
   std::vector<int64_t> valueset;  // ValueSet = ValueSpace \cup {0}, sorted
   u64 n_init;                     // number of initial states
   int max_new_per_state;          // upper bound on distinct successors of one state
+  std::shared_ptr<UserProg> user;  // the user invariants' program (user_inv.h), or null
+  std::string user_defs;          // their text (tlcg_model.user_defs)
 };
+
+// Compiles the user invariants `names` (definitions of m.user_defs) into *P
+// (user_inv.cpp); false with a message otherwise.
+bool compile_user_invariants(const tlcg_model& m, const HostModel& hm, const std::vector<std::string>& names,
+                             UserProg* P, std::string* err);
+std::vector<std::string> user_def_names(const char* text);
+
+// every invariant of the cfg, the user's included: -1, else (index << 1) | is_error
+template <typename W>
+int host_check_all(const HostModel& hm, W s) {
+  return hm.user ? check_invariants_all(hm.L, *hm.user, s) : check_invariants(hm.L, s);
+}
 
 // Builds the layout; returns false with a TLC-style message on an ASSUME
 // failure (compaction.tla:25-35) or on constants this build cannot pack.

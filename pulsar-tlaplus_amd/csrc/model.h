@@ -86,7 +86,9 @@ struct Layout {
   int32_t retain, producer, consumer, term_ok, check_deadlock;
   int32_t ord_bits;            // bits of a successor ordinal (Next position)
   int32_t n_inv;
-  int32_t inv[8];              // invariant kinds in cfg order (compaction.cfg:25-31)
+  int32_t inv[8];              // invariant kinds in cfg order (compaction.cfg:25-31); >= INV_USER: user_inv.h
+  int32_t defer_inv;           // 1: the cfg has user invariants -- the level's check kernel evaluates
+                               // every invariant (check_invariants_all), the expand kernels none
   u64 msgs_mask;               // bits holding `messages` (low word)
   u64 led_present_mask;        // bit0 of every ledger slot (low word)
   u64 msgs_mask_hi;            // the same masks' bits 64..127 (wide layouts)
@@ -431,6 +433,7 @@ TLCG_HD int eval_invariant(const Layout& L, int kind, W s) {
 // (index << 1) | is_error.
 template <typename W>
 TLCG_HD int check_invariants(const Layout& L, W s) {
+  if (L.defer_inv) return -1;  // user invariants: k_user_check (user_inv.h) checks them all, in cfg order
   for (int q = 0; q < L.n_inv; ++q) {
     int r = eval_invariant(L, L.inv[q], s);
     if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);

@@ -69,6 +69,24 @@ __device__ __forceinline__ int owner_of(W s, u64 owner_mask, int world) {
 // overflow flag of a failed FPSet insert
 __device__ __forceinline__ unsigned ovf_of(int r) { return r == -2 ? (unsigned)OVF_WIDE_SPIN : (unsigned)OVF_FPSET; }
 
+// ---- user invariants (user_inv.h): every invariant of the cfg, in its
+// order, on each state of a new level (the expand kernels check none when the
+// cfg has user invariants, Layout.defer_inv).  The event key is the state's
+// first-discovery key -- its parent reference without the rank, or its Init
+// index on level 0 -- as the expand kernels' (kernels.h make_event), so the
+// least event of a level is TLC's first error there in TLC-order mode.
+template <typename W>
+__global__ __launch_bounds__(BLOCK) void k_user_check(Layout L, const UserProg* __restrict__ P,
+                                                      const W* __restrict__ states, const u64* __restrict__ parents,
+                                                      u64 n, int level0, unsigned long long* ev) {
+  const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const int c = check_invariants_all(L, *P, states[i]);
+  if (c < 0) return;
+  const u64 dkey = level0 ? i : (parents[i] & ((1ull << 56) - 1));
+  atomicMin(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+}
+
 // ---- Init (compaction.tla:188-202), world == 1: initial state idx goes to
 // store position idx, which is also TLC's enumeration order.
 template <typename W>
@@ -759,6 +777,9 @@ struct tlcg_ctx {
   tlcg_model model;
   tlcg_opts opts;
   HostModel hm;
+  std::string user_defs;                 // model.user_defs points here (tlcg_create copies the caller's text)
+  UserProg* d_prog = nullptr;            // the user invariants' program on the device (user_inv.h)
+  unsigned long long* d_uev = nullptr;   // k_user_check's event (min)
   int words = 1;  // u64 words per state: 1, or 2 for wide layouts (> 63 bits)
   int device = 0;
   hipStream_t stream = nullptr;
@@ -1743,7 +1764,7 @@ bool component_applicable(const tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   const int mb = L.msg_sh + L.N * L.mw;
   return !L.producer && !c->opts.tlc_order && c->closed && L.bits <= 63 && L.bits - mb <= 32 && L.N <= 8 &&
-         c->hm.n_init < (1ull << 36);
+         c->hm.n_init < (1ull << 36) && !c->hm.user;
 }
 
 bool comp_scratch(tlcg_ctx* c, u64 n) {
@@ -1906,7 +1927,7 @@ bool tree_applicable(const tlcg_ctx* c) {
   const char* tv = std::getenv("TLCG_TREE");
   return L.producer && !(tv && std::atoi(tv) == 0) && !c->opts.tlc_order && c->opts.world == 1 && c->words == 1 &&
          L.bits - mb <= 31 && L.N >= 1 && L.N <= 8 && !c->opts.outdegree && L.nkv >= 1 && c->hm.n_init >= 1 &&
-         !c->opts.device_store_cap && !c->opts.fpset_spill;
+         !c->opts.device_store_cap && !c->opts.fpset_spill && !c->hm.user;
 }
 
 // the closed mode (tree.h): no Producer, a closed partition, components the
@@ -1917,7 +1938,8 @@ bool tree_closed_applicable(const tlcg_ctx* c) {
   const char* tv = std::getenv("TLCG_TREE");
   return !L.producer && !(tv && std::atoi(tv) == 0) && c->closed && !c->opts.tlc_order && !c->opts.outdegree &&
          code_bits(L) <= 31 && L.N >= 1 && L.N <= 8 && (c->words == 1 || c->words == 2) &&
-         c->hm.n_init >= 1 && c->hm.n_init < (1ull << 40) && !c->opts.device_store_cap && !c->opts.fpset_spill;
+         c->hm.n_init >= 1 && c->hm.n_init < (1ull << 40) && !c->opts.device_store_cap && !c->opts.fpset_spill &&
+         !c->hm.user;
 }
 
 // Run the component tree.  Producer modelled: every layer, chunks of 384
@@ -2078,6 +2100,28 @@ int run_tree(tlcg_ctx* c) {
   return 0;  // a component past the largest chunk
 }
 
+// the least user-invariant event of the new level [g0, g0 + n) (NO_EVENT: none,
+// or no user invariants); ~0ull - 1 on a launch error
+u64 user_check_level(tlcg_ctx* c, u64 g0, u64 n, bool level0) {
+  if (!c->hm.user || !n) return NO_EVENT;
+  unsigned long long h = NO_EVENT;
+  if (hipMemcpyAsync(c->d_uev, &h, sizeof h, hipMemcpyHostToDevice, c->stream) != hipSuccess) return ~0ull - 1;
+  const unsigned g = grid_for(n, BLOCK, 0x7fffffffu);
+  if (c->words == 1)
+    k_user_check<u64><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, dev_state(c, g0), dev_parent(c, g0), n,
+                                                   level0 ? 1 : 0, c->d_uev);
+  else
+    k_user_check<u128><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, (const u128*)dev_state(c, g0),
+                                                    dev_parent(c, g0), n, level0 ? 1 : 0, c->d_uev);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(&h, c->d_uev, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    c->err = "user-invariant check failed";
+    return ~0ull - 1;
+  }
+  return h;
+}
+
 bool run_init(tlcg_ctx* c) {
   c->engine = TLCG_ENGINE_GLOBAL;
   const HostModel& hm = c->hm;
@@ -2151,7 +2195,10 @@ bool run_init(tlcg_ctx* c) {
   // partitioned ranks keep every level (possibly empty) so that level d is
   // the same BFS level on every rank; termination is decided globally.
   if (n_new || world > 1) c->level_base.push_back(n_new);
-  if (c->h_ctr->event != NO_EVENT) return resolve_event(c, c->h_ctr->event, 0);
+  const u64 uev = user_check_level(c, 0, n_new, true);
+  if (uev == ~0ull - 1) return false;
+  const u64 ev = std::min<u64>(c->h_ctr->event, uev);
+  if (ev != NO_EVENT) return resolve_event(c, ev, 0);
   if (!n_new && world == 1) c->status = TLCG_DONE;
   return true;
 }
@@ -2341,7 +2388,10 @@ bool step_level(tlcg_ctx* c) {
   c->generated += c->h_ctr->generated;
   if (c->outdeg_valid && !add_child_runs(c, d, n_new, F)) return false;
   if (n_new) c->level_base.push_back(d + n_new);
-  if (c->h_ctr->event != NO_EVENT) return resolve_event(c, c->h_ctr->event, depth);
+  const u64 uev = user_check_level(c, d, n_new, false);
+  if (uev == ~0ull - 1) return false;
+  const u64 ev = std::min<u64>(c->h_ctr->event, uev);
+  if (ev != NO_EVENT) return resolve_event(c, ev, depth);
   if (!n_new) c->status = TLCG_DONE;
   return true;
 }
@@ -2371,6 +2421,18 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
   if (!build_model(*m, &c->hm, &c->err)) {
     *out = c;
     return -3;
+  }
+  c->user_defs = m->user_defs ? m->user_defs : "";
+  c->model.user_defs = m->user_defs ? c->user_defs.c_str() : nullptr;
+  if (c->hm.user && c->opts.world != 1) {
+    c->err = "user invariants are checked on one rank (world 1)";
+    *out = c;
+    return -2;
+  }
+  if (c->hm.user && (c->opts.engine == TLCG_ENGINE_COMPONENT || c->opts.engine == TLCG_ENGINE_TREE)) {
+    c->err = "user invariants are checked by the global engine";
+    *out = c;
+    return -2;
   }
   c->words = state_words(c->hm.L);
   // partition key: `messages` alone when it is immutable (no Producer), so a
@@ -2423,6 +2485,12 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
     c->err = "counter allocation failed";
     return -4;
   }
+  if (c->hm.user && (hipMalloc((void**)&c->d_prog, sizeof(UserProg)) != hipSuccess ||
+                     hipMemcpy(c->d_prog, c->hm.user.get(), sizeof(UserProg), hipMemcpyHostToDevice) != hipSuccess ||
+                     hipMalloc((void**)&c->d_uev, sizeof(unsigned long long)) != hipSuccess)) {
+    c->err = "user-invariant program upload failed";
+    return -4;
+  }
   if (c->opts.state_capacity && !ensure_store(c, c->opts.state_capacity)) return -5;
   if (c->opts.log2_fpset_slots > 0 && !rebuild_fpset(c, c->opts.log2_fpset_slots, 0)) return -5;
   return 0;
@@ -2455,6 +2523,8 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_inbox);
   hipFree(c->d_ctr);
   hipFree(c->d_aux);
+  hipFree(c->d_prog);
+  hipFree(c->d_uev);
   jit_release(&c->jit);
   hipFree(c->d_comp);
   hipFree(c->d_tree_dep);
@@ -2836,8 +2906,14 @@ struct CkptHeader {
   double kernel_ms, expand_ms;
 };
 const char kCkptMagic[8] = {'T', 'L', 'C', 'G', 'C', 'K', 'P', '1'};
+// the checkpoint's own format version (CkptHeader.abi), separate from the C
+// ABI's: 2 = header, tlcg_model, levels, states, parents (rounds 1-2);
+// 3 = the same with tlcg_model.user_defs as a length-prefixed text after the
+// model (a C-ABI bump no longer orphans checkpoints)
+constexpr int32_t kCkptFormat = 3;
 
 bool same_constants(const tlcg_model& a, const tlcg_model& b) {
+  if (std::string(a.user_defs ? a.user_defs : "") != std::string(b.user_defs ? b.user_defs : "")) return false;
   if (a.msg_sent_limit != b.msg_sent_limit || a.compaction_times_limit != b.compaction_times_limit ||
       a.consume_times_limit != b.consume_times_limit || a.max_crash_times != b.max_crash_times ||
       a.model_consumer != b.model_consumer || a.model_producer != b.model_producer ||
@@ -2906,7 +2982,7 @@ int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
   CkptHeader h;
   std::memset(&h, 0, sizeof h);
   std::memcpy(h.magic, kCkptMagic, 8);
-  h.abi = TLCG_ABI_VERSION;
+  h.abi = kCkptFormat;
   h.words = c->words;
   h.rank = c->opts.rank;
   h.world = c->opts.world;
@@ -2928,7 +3004,11 @@ int tlcg_checkpoint(tlcg_ctx* c, const char* path) {
   c->err.clear();
   void* stage = nullptr;
   bool ok = hipHostMalloc(&stage, kStage) == hipSuccess;
-  ok = ok && std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(&c->model, sizeof c->model, 1, f) == 1 &&
+  tlcg_model mw = c->model;
+  mw.user_defs = nullptr;  // (the text follows the model)
+  const uint64_t ulen = c->user_defs.size();
+  ok = ok && std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(&mw, sizeof mw, 1, f) == 1 &&
+       std::fwrite(&ulen, 8, 1, f) == 1 && std::fwrite(c->user_defs.data(), 1, ulen, f) == ulen &&
        std::fwrite(c->level_base.data(), 8, c->level_base.size(), f) == c->level_base.size();
   // spilled levels from their host chunks, the rest from the device
   for (const auto& hc : c->hchunks) ok = ok && std::fwrite(hc.st, 8 * c->words, hc.n, f) == hc.n;
@@ -2961,7 +3041,27 @@ int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st) {
     c->err = std::string(path) + " is not a tlcgpu checkpoint";
     return -3;
   }
-  if (h.abi != TLCG_ABI_VERSION || !same_constants(m, c->model) || h.words != c->words || h.rank != c->opts.rank ||
+  if (h.abi != kCkptFormat) {
+    std::fclose(f);
+    c->err = "the checkpoint is in format " + std::to_string(h.abi) + "; this build reads format " +
+             std::to_string(kCkptFormat);
+    return -4;
+  }
+  uint64_t ulen = 0;
+  std::string udefs;
+  if (std::fread(&ulen, 8, 1, f) != 1 || ulen > (64u << 20)) {
+    std::fclose(f);
+    c->err = "checkpoint file is truncated or corrupt";
+    return -3;
+  }
+  udefs.resize(ulen);
+  if (ulen && std::fread(&udefs[0], 1, ulen, f) != ulen) {
+    std::fclose(f);
+    c->err = "checkpoint file is truncated or corrupt";
+    return -3;
+  }
+  m.user_defs = ulen ? udefs.c_str() : nullptr;
+  if (!same_constants(m, c->model) || h.words != c->words || h.rank != c->opts.rank ||
       h.world != c->opts.world || h.tlc_order != c->opts.tlc_order ||
       (h.world > 1 && h.partition != c->opts.partition) || h.n_levels < 1) {
     std::fclose(f);

@@ -27,6 +27,9 @@ namespace tlcg {
 // fewer, so one component per 64-lane wavefront leaves most lanes idle and
 // pays the scalar (exec-mask, loop) instructions once per state; G groups
 // share them.
+#ifndef TLCG_TREE_MULT  // the slot hash's multiplier (multiply-shift)
+#define TLCG_TREE_MULT 0x9E3779B1u
+#endif
 #ifndef TLCG_TREE_TSCALE_CLOSED
 #define TLCG_TREE_TSCALE_CLOSED 100
 #endif
@@ -115,8 +118,8 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   auto insert = [&](bool pred, uint32_t key, u64 pref, int dd) {
     bool isnew = false;
     if (pred) {
-      unsigned s = TPOW2 ? (key * 0x9E3779B1u) >> (32 - log2t)
-                         : (unsigned)(((unsigned long long)(key * 0x9E3779B1u) * (unsigned)TT) >> 32);
+      unsigned s = TPOW2 ? (key * (uint32_t)TLCG_TREE_MULT) >> (32 - log2t)
+                         : (unsigned)(((unsigned long long)(key * (uint32_t)TLCG_TREE_MULT) * (unsigned)TT) >> 32);
       for (int p = 0; p < TT; ++p) {
         const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
         // Producer mode: the probe loop with one exit (P8 2.07 -> 1.99 ms);
@@ -157,8 +160,12 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       }
       par[pos] = pref == NO_PARENT ? NO_PARENT : (a.rank_tag | pref);
       if constexpr (CLOSED) {
+#ifndef TLCG_TREE_NO_STORE  // (experiment only: what the state words cost)
         st[pos] = code_word<W>(L, kc, msgs, key);
+#endif
+#ifndef TLCG_TREE_NO_INV  // (experiment only: what the invariants cost)
         if (check_invariants_cb(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
+#endif
       } else {
         st[pos] = msgs | ((u64)key << mb);
         dp[pos] = (uint8_t)dd;  // (read by the next layer)

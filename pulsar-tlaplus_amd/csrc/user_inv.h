@@ -1,0 +1,189 @@
+// pulsar-tlaplus_amd/csrc/user_inv.h -- invariants a user adds to the module
+// (BASELINE config 5: "mutated compaction.tla with an injected invariant
+// violation at depth"), compiled on the host (user_inv.cpp) from their TLA+
+// text into a small register program over the packed state word, and run
+// by this interpreter on the host and on the GPU (k_user_check, tlcgpu.hip).
+//
+// A user invariant is a state predicate over the spec's variables
+// (compaction.tla:57-70) and constants (:10-18, :38-54): the compiler resolves
+// every composite value (message records, sequences, the ledger function,
+// the cursor and phaseOneResult records, sets) statically, so the program
+// only moves 64-bit integers: field reads of the packed state (model.h
+// layout), arithmetic, comparisons, bit operations on the ledgers' position
+// masks, and jumps for short-circuit logic, IF, quantifiers and CHOOSE.
+// Evaluation errors (out-of-domain application, a field of Nil, an empty
+// CHOOSE, ...) end the program with EV_ERROR, as TLC's evaluator would.
+#pragma once
+#if !defined(__HIPCC_RTC__)
+#include "model.h"
+#endif
+
+namespace tlcg {
+
+constexpr int UI_MAXINS = 4096;  // instructions over all user invariants of a model (32 KB, device memory)
+constexpr int UI_MAXREG = 64;    // registers (int64) of the program
+constexpr int UI_MAXSET = 64;    // KeySet / ValueSet elements (incl. NullKey / NullValue)
+constexpr int INV_USER = 16;     // tlcg_model.invariants: INV_USER + k = the k-th user invariant
+
+// model values as integers (compactorState's phases and Nil); disjoint from
+// every integer the spec's variables take, and compared only with each other
+enum { UV_NIL = -1000, UV_PHASE0 = -999 /* + phase (compaction.tla:39-44) */ };
+
+enum UOp : uint8_t {
+  U_LDI,     // r[a] = imm
+  U_MOV,     // r[a] = r[b]
+  U_LEN,     // r[a] = Len(messages)
+  U_MKEY,    // r[a] = messages[r[b]].key (the key's value; r[b] in 1..N)
+  U_MVAL,    // r[a] = messages[r[b]].value
+  U_PHASE,   // r[a] = compactorState (UV_PHASE0 + phase)
+  U_P1R,     // r[a] = phaseOneResult.readPosition, 0 = Nil
+  U_HZ,      // r[a] = compactionHorizon
+  U_CTX,     // r[a] = compactedTopicContext
+  U_CRASH,   // r[a] = crashTimes
+  U_CURP,    // r[a] = cursor # Nil
+  U_CURH,    // r[a] = cursor.compactionHorizon (cursor not Nil)
+  U_CURC,    // r[a] = cursor.compactedTopicContext
+  U_LEDP,    // r[a] = compactedLedgers[r[b]] # Nil (r[b] in 1..C)
+  U_LEDM,    // r[a] = position mask of compactedLedgers[r[b]] (bit p-1: messages[p])
+  U_LFK,     // r[a] = max i in 1..r[c] with messages[i].key = r[b], 0 if none
+  U_ADD, U_SUB, U_MUL,
+  U_DIV,     // r[a] = r[b] \div r[c] (floor; r[c] > 0 checked by the program)
+  U_MOD,     // r[a] = r[b] % r[c] (0..r[c]-1)
+  U_NEG,     // r[a] = -r[b]
+  U_EQ, U_NE, U_LT, U_LE,  // r[a] = r[b] op r[c] (0/1)
+  U_NOT,     // r[a] = !r[b]
+  U_AND, U_OR,  // r[a] = r[b] & r[c], r[b] | r[c] (on 0/1)
+  U_ADDI,    // r[a] = r[b] + imm
+  U_BIT,     // r[a] = (r[b] >> (r[c] - 1)) & 1 (r[c] in 1..63)
+  U_POPC,    // r[a] = popcount(r[b])
+  U_NTH,     // r[a] = position of the r[c]-th set bit of r[b] (1-based), 0 if fewer
+  U_MASK,    // r[a] = (1 << r[b]) - 1 (r[b] in 0..62)
+  U_KIN,     // r[a] = r[b] \in KeySet (imm 0) / ValueSet (imm 1)
+  U_KAT,     // r[a] = the r[b]-th (0-based) element of KeySet in ascending order (imm 0), ValueSet (imm 1)
+  U_JMP,     // pc = imm
+  U_JZ,      // if (!r[a]) pc = imm
+  U_JNZ,     // if (r[a]) pc = imm
+  U_ERR,     // evaluation error
+  U_RET,     // return r[a] ? TRUE : FALSE
+};
+
+struct UInsn {
+  uint8_t op, a, b, c;
+  int32_t imm;
+};
+
+struct UserProg {
+  int32_t n_user;                 // user invariants
+  int32_t n_ins;
+  int32_t entry[8];               // first instruction of user invariant k
+  int32_t nk, nv;                 // |KeySet|, |ValueSet|
+  int32_t keyval[UI_MAXSET];      // key index -> value (model.h: index 0 = NullKey = 0)
+  int32_t valval[UI_MAXSET];      // value index -> value
+  int32_t keysorted[UI_MAXSET];   // KeySet in ascending order
+  int32_t valsorted[UI_MAXSET];   // ValueSet in ascending order
+  UInsn ins[UI_MAXINS];
+};
+
+// Runs user invariant k on state s: EV_TRUE / EV_FALSE / EV_ERROR.
+template <typename W>
+TLCG_HD int eval_user(const Layout& L, const UserProg& P, int k, W s) {
+  long long r[UI_MAXREG];
+  int pc = P.entry[k];
+  for (int steps = 0; steps < (1 << 20); ++steps) {  // (a program is a DAG plus bounded loops)
+    const UInsn in = P.ins[pc++];
+    switch (in.op) {
+      case U_LDI: r[in.a] = in.imm; break;
+      case U_MOV: r[in.a] = r[in.b]; break;
+      case U_LEN: r[in.a] = st_len(L, s); break;
+      case U_MKEY: r[in.a] = P.keyval[st_key(L, s, (int)r[in.b]) & (UI_MAXSET - 1)]; break;
+      case U_MVAL: r[in.a] = P.valval[st_val(L, s, (int)r[in.b]) & (UI_MAXSET - 1)]; break;
+      case U_PHASE: r[in.a] = UV_PHASE0 + st_phase(L, s); break;
+      case U_P1R: r[in.a] = st_p1r(L, s); break;
+      case U_HZ: r[in.a] = st_hz(L, s); break;
+      case U_CTX: r[in.a] = st_ctx(L, s); break;
+      case U_CRASH: r[in.a] = st_crash(L, s); break;
+      case U_CURP: r[in.a] = cur_present(L, s); break;
+      case U_CURH: r[in.a] = cur_h(L, s); break;
+      case U_CURC: r[in.a] = cur_c(L, s); break;
+      case U_LEDP: r[in.a] = led_present(L, s, (int)r[in.b]); break;
+      case U_LEDM: r[in.a] = (long long)led_mask(L, s, (int)r[in.b]); break;
+      case U_LFK: {
+        long long best = 0;
+        for (int i = 1; i <= (int)r[in.c] && i <= L.N; ++i)
+          if (P.keyval[st_key(L, s, i) & (UI_MAXSET - 1)] == r[in.b]) best = i;
+        r[in.a] = best;
+        break;
+      }
+      case U_ADD: r[in.a] = r[in.b] + r[in.c]; break;
+      case U_SUB: r[in.a] = r[in.b] - r[in.c]; break;
+      case U_MUL: r[in.a] = r[in.b] * r[in.c]; break;
+      case U_DIV: {
+        const long long q = r[in.b] / r[in.c];
+        r[in.a] = (r[in.b] % r[in.c] != 0 && ((r[in.b] < 0) != (r[in.c] < 0))) ? q - 1 : q;
+        break;
+      }
+      case U_MOD: {
+        const long long m = r[in.b] % r[in.c];
+        r[in.a] = m < 0 ? m + r[in.c] : m;
+        break;
+      }
+      case U_NEG: r[in.a] = -r[in.b]; break;
+      case U_EQ: r[in.a] = r[in.b] == r[in.c]; break;
+      case U_NE: r[in.a] = r[in.b] != r[in.c]; break;
+      case U_LT: r[in.a] = r[in.b] < r[in.c]; break;
+      case U_LE: r[in.a] = r[in.b] <= r[in.c]; break;
+      case U_NOT: r[in.a] = !r[in.b]; break;
+      case U_AND: r[in.a] = r[in.b] & r[in.c]; break;
+      case U_OR: r[in.a] = r[in.b] | r[in.c]; break;
+      case U_ADDI: r[in.a] = r[in.b] + in.imm; break;
+      case U_BIT: r[in.a] = (r[in.c] >= 1 && r[in.c] <= 63) ? (r[in.b] >> (r[in.c] - 1)) & 1 : 0; break;
+      case U_POPC: r[in.a] = popcount64((u64)r[in.b]); break;
+      case U_NTH: {
+        u64 m = (u64)r[in.b];
+        long long j = r[in.c], pos = 0;
+        for (int p = 1; p <= 63 && m; ++p, m >>= 1)
+          if ((m & 1) && --j == 0) {
+            pos = p;
+            break;
+          }
+        r[in.a] = j > 0 || r[in.c] < 1 ? 0 : pos;
+        break;
+      }
+      case U_MASK: r[in.a] = (long long)((1ull << (r[in.b] & 63)) - 1); break;
+      case U_KIN: {
+        const int n = in.imm ? P.nv : P.nk;
+        const int32_t* t = in.imm ? P.valsorted : P.keysorted;
+        long long f = 0;
+        for (int i = 0; i < n && i < UI_MAXSET; ++i) f |= t[i] == r[in.b];
+        r[in.a] = f;
+        break;
+      }
+      case U_KAT: {
+        const int i = (int)r[in.b] & (UI_MAXSET - 1);
+        r[in.a] = in.imm ? P.valsorted[i] : P.keysorted[i];
+        break;
+      }
+      case U_JMP: pc = in.imm; break;
+      case U_JZ: if (!r[in.a]) pc = in.imm; break;
+      case U_JNZ: if (r[in.a]) pc = in.imm; break;
+      case U_ERR: return EV_ERROR;
+      case U_RET: return r[in.a] ? EV_TRUE : EV_FALSE;
+      default: return EV_ERROR;
+    }
+  }
+  return EV_ERROR;
+}
+
+// Every invariant of the cfg in its order -- the spec's own (model.h) and the
+// user's: -1 if all hold, else (index << 1) | is_error (as check_invariants).
+template <typename W>
+TLCG_HD int check_invariants_all(const Layout& L, const UserProg& P, W s) {
+  for (int q = 0; q < L.n_inv; ++q) {
+    const int kind = L.inv[q];
+    const int r = kind >= INV_USER ? eval_user(L, P, kind - INV_USER, s) : eval_invariant(L, kind, s);
+    if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
+  }
+  return -1;
+}
+
+}  // namespace tlcg

@@ -22,6 +22,7 @@ MAX_SET = 63
 MAX_INV = 8
 
 INVARIANTS = ("TypeSafe", "CompactedLedgerLeak", "CompactionHorizonCorrectness", "DuplicateNullKeyMessage")
+INV_USER = 16  # TLCG_INV_USER: invariants[q] = INV_USER + j names the j-th user definition
 ACTIONS = ("Producer", "CompactorPhaseOne", "CompactorPhaseTwoWrite", "CompactorPhaseTwoUpdateContext",
            "CompactorPhaseTwoUpdateHorizon", "CompactorPhaseTwoPersistCusror", "CompactorPhaseTwoDeleteLedger",
            "BrokerCrash", "Consumer", "Terminating")
@@ -37,7 +38,8 @@ class tlcg_model(C.Structure):
                 ("retain_null_key", C.c_uint8), ("check_deadlock", C.c_uint8),
                 ("n_keys", C.c_int32), ("n_values", C.c_int32),
                 ("keys", C.c_int64 * MAX_SET), ("values", C.c_int64 * MAX_SET),
-                ("n_invariants", C.c_int32), ("invariants", C.c_int32 * MAX_INV)]
+                ("n_invariants", C.c_int32), ("invariants", C.c_int32 * MAX_INV),
+                ("user_defs", C.c_char_p)]
 
 
 class tlcg_opts(C.Structure):
@@ -120,6 +122,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_host_init_state_words": (C.c_int, [M, U64, C.POINTER(U64)]),
         "tlcg_host_successors_words": (C.c_int, [M, C.POINTER(U64), C.POINTER(U64), C.POINTER(I32), I32]),
         "tlcg_host_check_invariants_words": (C.c_int, [M, C.POINTER(U64)]),
+        "tlcg_host_check_invariants_batch": (C.c_int, [M, C.POINTER(U64), U64, C.POINTER(I32)]),
         "tlcg_trace_words": (C.c_int, [P, C.POINTER(U64), C.POINTER(I32), I32, C.POINTER(I32)]),
         "tlcg_state_at_words": (C.c_int, [P, U64, C.POINTER(U64), C.POINTER(U64)]),
         "tlcg_copy_states_words": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
@@ -162,6 +165,26 @@ class Model:
     value_space: Sequence[int] = (1, 2)
     invariants: Sequence[str] = ("TypeSafe", "CompactionHorizonCorrectness")
     check_deadlock: bool = True
+    # definitions added to the module (BASELINE config 5): "Name" or
+    # "Name(p1, p2)" -> TLA+ body text; INVARIANTS may name the zero-argument
+    # ones (include/tlcgpu.h tlcg_model.user_defs).  A name here shadows the
+    # spec's invariant of that name.
+    user_defs: Optional[dict] = None
+
+    def user_defs_text(self) -> Optional[str]:
+        """tlcg_model.user_defs: a "@@DEF name params" header line per definition, then its body"""
+        if not self.user_defs:
+            return None
+        out = []
+        for head, body in self.user_defs.items():
+            name, _, rest = head.partition("(")
+            params = [p.strip() for p in rest.rstrip(")").split(",") if p.strip()]
+            out.append("@@DEF " + " ".join([name.strip()] + params))
+            out.append(body)
+        return "\n".join(out) + "\n"
+
+    def user_names(self) -> List[str]:
+        return [h.partition("(")[0].strip() for h in (self.user_defs or {})]
 
     def to_c(self) -> tlcg_model:
         m = tlcg_model()
@@ -184,10 +207,17 @@ class Model:
         if len(self.invariants) > MAX_INV:
             raise ValueError("too many invariants")
         m.n_invariants = len(self.invariants)
+        users = self.user_names()
         for i, name in enumerate(self.invariants):
-            if name not in INVARIANTS:
+            if name in users:
+                m.invariants[i] = INV_USER + users.index(name)
+            elif name in INVARIANTS:
+                m.invariants[i] = INVARIANTS.index(name)
+            else:
                 raise ValueError(f"unknown invariant {name}")
-            m.invariants[i] = INVARIANTS.index(name)
+        text = self.user_defs_text()
+        if text is not None:
+            m.user_defs = text.encode()  # (ctypes keeps the bytes alive with the struct)
         return m
 
     def oracle_args(self) -> List[str]:
@@ -272,6 +302,20 @@ def host_component_selfcheck(model: Model, first: int, n: int) -> int:
     return load_library().tlcg_host_component_selfcheck(C.byref(m), C.c_uint64(first), C.c_uint64(n))
 
 
+def host_check_invariants_batch(model: Model, states: Sequence[int]) -> List[int]:
+    """check_invariants of every state (-1: all hold, else index << 1 | is_error), one model build"""
+    m = model.to_c()
+    w = state_words(model)
+    buf = (C.c_uint64 * (len(states) * w))()
+    for i, s in enumerate(states):
+        for k in range(w):
+            buf[i * w + k] = (s >> (64 * k)) & 0xFFFFFFFFFFFFFFFF
+    out = (C.c_int32 * max(1, len(states)))()
+    if load_library().tlcg_host_check_invariants_batch(C.byref(m), buf, len(states), out) != 0:
+        raise ValueError(check_model(model) or "bad model")
+    return list(out)[:len(states)]
+
+
 def host_check_invariants(model: Model, state: int) -> int:
     m = model.to_c()
     return load_library().tlcg_host_check_invariants_words(C.byref(m), _to_words(state, state_words(model)))
@@ -299,7 +343,7 @@ class Liveness:
 
 def check_termination(model: Model, fairness: str = "none", device: int = 0, state_capacity: int = 0,
                       log2_fpset_slots: int = 0) -> Liveness:
-    """TLC's liveness check of PROPERTY Termination under Spec (fairness
+    r"""TLC's liveness check of PROPERTY Termination under Spec (fairness
     "none") or Spec /\ WF_vars(Next) ("wf"), through tlcg_check_termination."""
     lib = load_library()
     m = model.to_c()

@@ -1,0 +1,127 @@
+"""Shared fixtures of the user-invariant tests (BASELINE config 5): the
+definitions a user adds to compaction.tla, and a synchronized BFS that pairs
+every reachable packed state of the product with the Python oracle's value
+of the same state (both enumerate Init and Next in TLC's order)."""
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pulsar-tlaplus_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle_py  # noqa: E402
+import tlcgpu as T  # noqa: E402
+
+REF_TLA = "/root/reference/compaction.tla"
+
+# helper definitions restated for the tests (the CLI takes them from the .tla)
+HELPERS = {
+    "NullKey": "0",
+    "KeySet": "KeySpace \\cup {NullKey}",
+    "ValueSet": "ValueSpace \\cup {0}",
+    "MaxId(s)": "CHOOSE x \\in s : \\A y \\in s : x >= y",
+    "MaxLedger": "IF \\E i \\in 1..CompactionTimesLimit : compactedLedgers[i] # Nil\n"
+                 "THEN MaxId({i \\in 1..CompactionTimesLimit : compactedLedgers[i] # Nil})\n"
+                 "ELSE 0",
+}
+
+# name -> body: invariants exercising the supported language; some hold on
+# the shipped constants, some fail at depth, some raise evaluation errors
+CASES = {
+    "LedgerCount": "Cardinality({i \\in 1..CompactionTimesLimit : compactedLedgers[i] # Nil}) <= 2",
+    "ContextBound": "compactedTopicContext < 3",
+    "CursorAfterContext": "/\\ cursor # Nil => cursor.compactedTopicContext <= compactedTopicContext + 1\n"
+                          "/\\ crashTimes \\in 0..MaxCrashTimes",
+    "PhaseKnown": "compactorState \\in {Compactor_In_PhaseOne, Compactor_In_PhaseTwoWrite,\n"
+                  "                   Compactor_In_PhaseTwoUpdateContext, Compactor_In_PhaseTwoUpdateHorizon,\n"
+                  "                   Compactor_In_PhaseTwoPersistCusror, Compactor_In_PhaseTwoDeleteLedger}",
+    "MaxLedgerBound": "MaxLedger <= 2 \\/ compactorState # Compactor_In_PhaseTwoUpdateContext",
+    "LatestIsLast": "phaseOneResult # Nil =>\n"
+                    "  \\A k \\in DOMAIN phaseOneResult.latestForKey :\n"
+                    "    /\\ messages[phaseOneResult.latestForKey[k]].key = k\n"
+                    "    /\\ \\A i \\in 1..phaseOneResult.readPosition :\n"
+                    "         messages[i].key = k => i <= phaseOneResult.latestForKey[k]",
+    "LedgerSorted": "\\A l \\in 1..CompactionTimesLimit :\n"
+                    "  compactedLedgers[l] # Nil =>\n"
+                    "    \\A a \\in 1..Len(compactedLedgers[l]) : \\A b \\in 1..Len(compactedLedgers[l]) :\n"
+                    "      a < b => compactedLedgers[l][a].id < compactedLedgers[l][b].id",
+    "LetChoose": "LET live == {i \\in 1..CompactionTimesLimit : compactedLedgers[i] # Nil}\n"
+                 "    top(s) == CHOOSE x \\in s : \\A y \\in s : x >= y\n"
+                 "IN  live # {} => top(live) >= compactedTopicContext",
+    "ArithCase": "CASE compactionHorizon = 0 -> (crashTimes * 2) % 3 \\in {0, 2}\n"
+                 "  [] OTHER -> compactionHorizon \\div 2 <= MessageSentLimit",
+    "NoDoubleCrashWrite": "~(crashTimes = MaxCrashTimes /\\ compactorState = Compactor_In_PhaseTwoWrite\n"
+                          "   /\\ compactedLedgers[2] # Nil)",
+    "ContextLedgerError": "Len(compactedLedgers[compactedTopicContext]) >= 0",
+    "KeysKnown": "\\A i \\in 1..Len(messages) : messages[i].key \\in KeySet /\\ messages[i].value \\in ValueSet",
+    "RecordEq": "cursor # Nil => cursor # [compactionHorizon |-> 0, compactedTopicContext |-> 0]",
+    "MessageRec": "\\A i \\in 1..Len(messages) :\n"
+                  "   messages[i] = [id |-> i, key |-> messages[i].key, value |-> messages[i].value]",
+    "SetMapKeys": "Cardinality({messages[i].key : i \\in 1..Len(messages)}) <= Len(messages)",
+    "HeadFirst": "Len(messages) > 0 => Head(messages).id = 1",
+}
+
+
+def model_with(names, **kw):
+    defs = dict(HELPERS)
+    defs.update({n: CASES[n] for n in names})
+    return T.Model(invariants=tuple(names), user_defs=defs, **kw)
+
+
+def oracle_model(m: T.Model, user_defs=None):
+    return oracle_py.Model(N=m.msg_sent_limit, C=m.compaction_times_limit, K=m.max_crash_times,
+                           keys=list(m.key_space), values=list(m.value_space), retain=m.retain_null_key,
+                           producer=m.model_producer, consumer=m.model_consumer, ctl=m.consume_times_limit,
+                           invariants=m.invariants, deadlock=m.check_deadlock,
+                           user_defs=user_defs if user_defs is not None else m.user_defs)
+
+
+def paired_states(m: T.Model, limit=None):
+    """(packed word, oracle state) for every reachable state, in BFS order"""
+    om = oracle_model(m)
+    inits = list(om.inits())
+    words = [T.host_init_state(m, i) for i in range(len(inits))]
+    seen = {}
+    order = []
+    queue = list(zip(words, inits))
+    head = 0
+    for w, o in queue:
+        if w not in seen:
+            seen[w] = o
+            order.append((w, o))
+    queue = list(order)
+    while head < len(queue):
+        w, o = queue[head]
+        head += 1
+        if limit and len(order) >= limit:
+            break
+        try:
+            ps = T.host_successors(m, w)
+        except RuntimeError:
+            continue
+        os_ = list(om.successors(o))
+        assert [a for a, _ in ps] == [oracle_py.ACTIONS[a] for a, _ in os_], (ps, os_)
+        for (_, t), (_, u) in zip(ps, os_):
+            if t in seen:
+                assert seen[t] == u
+                continue
+            seen[t] = u
+            order.append((t, u))
+            queue.append((t, u))
+    return order
+
+
+def ref_definition(name):
+    """body text of a top-level definition of the reference spec (read at test time, never stored)"""
+    lines = open(REF_TLA).read().split("\n")
+    for i, l in enumerate(lines):
+        m = re.match(r"^" + re.escape(name) + r"(\(.*\))? ==(.*)$", l)
+        if m:
+            out = [" " * (len(l) - len(m.group(2))) + m.group(2)]
+            for l2 in lines[i + 1:]:
+                if l2 and not l2[0].isspace():
+                    break
+                out.append(l2)
+            return (m.group(1) or ""), "\n".join(out).rstrip()
+    raise KeyError(name)
