@@ -129,6 +129,34 @@ class Model:
                 and (not self.consumer or cons == self.ctl)):  # Terminating, :205-214
             yield 9, s
 
+    # ---- TLC value syntax of a state (variables in declaration order, compaction.tla:57-70) ----
+    @staticmethod
+    def render(s):
+        msgs, led, cur, ph, p1r, hz, ctx, crash, cons = s
+        names = ("Compactor_In_PhaseOne", "Compactor_In_PhaseTwoWrite", "Compactor_In_PhaseTwoUpdateContext",
+                 "Compactor_In_PhaseTwoUpdateHorizon", "Compactor_In_PhaseTwoPersistCusror",
+                 "Compactor_In_PhaseTwoDeleteLedger")
+
+        def seq(ms):
+            return "<<" + ", ".join(f"[id |-> {i}, key |-> {k}, value |-> {v}]" for i, k, v in ms) + ">>"
+
+        if p1r is None:
+            p1 = "Nil"
+        else:
+            dom = [k for k, _ in p1r[1]]
+            f = ("<<" + ", ".join(str(v) for _, v in p1r[1]) + ">>" if dom == list(range(1, len(dom) + 1))
+                 else "(" + " @@ ".join(f"{k} :> {v}" for k, v in p1r[1]) + ")")
+            p1 = f"[latestForKey |-> {f}, readPosition |-> {p1r[0]}]"
+        return "\n".join([
+            "/\\ messages = " + seq(msgs),
+            "/\\ compactedLedgers = <<" + ", ".join("Nil" if l is None else seq(l) for l in led) + ">>",
+            "/\\ cursor = " + ("Nil" if cur is None else
+                               f"[compactedTopicContext |-> {cur[1]}, compactionHorizon |-> {cur[0]}]"),
+            "/\\ compactorState = " + names[ph],
+            "/\\ phaseOneResult = " + p1,
+            f"/\\ compactionHorizon = {hz}", f"/\\ compactedTopicContext = {ctx}",
+            f"/\\ crashTimes = {crash}", f"/\\ consumeTimes = {cons}"])
+
     # ---- invariants ----
     def ledger_at_ctx(self, s):
         led, ctx = s[1], s[6]

@@ -384,6 +384,8 @@ class Parser {
       return n;
     }
     if (t.k == Tok::OP && (t.s == "/\\" || t.s == "\\/" || t.s == "\\land" || t.s == "\\lor")) return junction();
+    if (t.k == Tok::OP && (t.s == "[]" || (t.s == "<" && peek(1).k == Tok::OP && peek(1).s == ">")))
+      fail("a temporal formula ([] or <>) is not a state predicate");
     if (t.k == Tok::OP && t.s == "(") {
       ++p_;
       fence_.push_back(-1);  // parentheses lift the bullet fence

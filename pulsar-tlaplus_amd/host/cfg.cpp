@@ -292,13 +292,16 @@ bool parse_module(const std::string& text, Module* out, std::string* err) {
         if (!isspace((unsigned char)s[b])) last = (int)b;
       if (last >= 0) { l1 = a; c1 = last; break; }
     }
-    std::string body;
+    std::string body, text;
     for (int a = l0; a <= l1 && c0 >= 0; ++a) {
       const std::string& s = L[(size_t)a];
       size_t from = a == l0 ? (size_t)c0 : 0;
       size_t to = a == l1 ? (size_t)c1 + 1 : s.size();
       if (from < s.size()) body += s.substr(from, std::min(to, s.size()) - from);
       body += '\n';
+      // the same lines with their columns (the first one's text before the body blanked)
+      if (from < s.size()) text += std::string(from, ' ') + s.substr(from, std::min(to, s.size()) - from);
+      text += '\n';
     }
     if (is_assume) {
       m.assume_l0 = l0 + 1; m.assume_c0 = c0 + 1; m.assume_l1 = l1 + 1; m.assume_c1 = c1 + 1;
@@ -314,6 +317,19 @@ bool parse_module(const std::string& text, Module* out, std::string* err) {
     d.name = name;
     d.line0 = l0 + 1; d.col0 = c0 + 1; d.line1 = l1 + 1; d.col1 = c1 + 1;
     d.norm = normalize(head + "==" + body);
+    d.text = text;
+    const size_t lp = head.find('('), rp = head.rfind(')');
+    if (lp != std::string::npos && rp != std::string::npos && rp > lp) {
+      std::string p;
+      for (char ch : head.substr(lp + 1, rp - lp - 1) + ",") {
+        if (ch == ',') {
+          if (!p.empty()) d.params.push_back(p);
+          p.clear();
+        } else if (!isspace((unsigned char)ch)) {
+          p += ch;
+        }
+      }
+    }
     m.by_name[d.name] = m.defs.size();
     m.defs.push_back(d);
   }
@@ -389,16 +405,32 @@ bool recognize_compaction(const Module& m, std::string* err) {
 static bool invariant_matches(const Module& m, const std::string& name) {
   const Def* d = m.find(name);
   if (!d) return false;
-  if (m.builtin) return true;
+  if (m.builtin && d->text.empty()) return true;  // (a definition added with -defs has its text)
   for (const Known& k : kKnown)
     if (name == k.name) return fnv1a(d->norm) == k.h;
   return false;
 }
 
+std::string user_defs_text(const Module& m, std::map<std::string, int>* index) {
+  std::string out;
+  int k = 0;
+  for (const Def& d : m.defs) {
+    if (d.name == "ASSUME" || d.name == "__DECLARATIONS__" || d.text.empty()) continue;
+    out += "@@DEF " + d.name;
+    for (const std::string& p : d.params) out += " " + p;
+    out += " @" + std::to_string(d.line0) + "\n" + d.text;
+    if (index) (*index)[d.name] = k;
+    ++k;
+  }
+  return out;
+}
+
 bool bind_model(const Config& cfg, const Module& mod, bool deadlock_flag, tlcg_model* m, std::string* err,
                 int* exit_code, int* fairness) {
   *m = tlcg_model();
-  *exit_code = 150;  // [TLC-ext] configuration/semantic error
+  // [TLC-ext] EC.ExitStatus.ERROR_CONFIG_PARSE (151): the cfg does not bind the
+  // module (150, ERROR_SPEC_PARSE, is the .tla's; 75 an evaluation error)
+  *exit_code = 151;
   static const char* kParams[] = {"MessageSentLimit", "CompactionTimesLimit", "ModelConsumer", "ConsumeTimesLimit",
                                   "KeySpace", "ValueSpace", "RetainNullKey", "MaxCrashTimes", "ModelProducer"};
   static const char* kModelValues[] = {"Nil", "Compactor_In_PhaseOne", "Compactor_In_PhaseTwoWrite",
@@ -581,9 +613,17 @@ bool bind_model(const Config& cfg, const Module& mod, bool deadlock_flag, tlcg_m
       return false;
     }
     if (id < 0 || !invariant_matches(mod, name)) {
-      *err = "Error: invariant " + name + " is not one this checker implements (" +
-             "TypeSafe, CompactedLedgerLeak, CompactionHorizonCorrectness, DuplicateNullKeyMessage as published).";
-      return false;
+      // an invariant the user added (or edited): compiled from its text by
+      // libtlcgpu (user_inv.cpp), which refuses what it cannot check exactly
+      static std::string defs;  // (tlcg_model.user_defs points here)
+      static std::map<std::string, int> index;
+      if (!m->user_defs) {
+        index.clear();
+        defs = user_defs_text(mod, &index);
+        m->user_defs = defs.c_str();
+      }
+      m->invariants[m->n_invariants++] = TLCG_INV_USER + index[name];
+      continue;
     }
     m->invariants[m->n_invariants++] = id;
   }

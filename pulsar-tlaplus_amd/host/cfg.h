@@ -38,6 +38,8 @@ struct Def {
   std::string name;
   int line0 = 0, col0 = 0, line1 = 0, col1 = 0;  // 1-based, inclusive: the body
   std::string norm;                               // whitespace/comment-normalized body
+  std::vector<std::string> params;                // operator parameters
+  std::string text;                               // the body as written, columns kept (user invariants)
 };
 
 struct Module {
@@ -63,7 +65,15 @@ Module builtin_module();
 // (operator bodies compared after normalization); lists differing ones.
 bool recognize_compaction(const Module& m, std::string* err);
 
+// The module's definitions in tlcg_model.user_defs form ("@@DEF name params
+// @line" + the body with its columns), for invariants the user added or
+// edited (BASELINE config 5); *index gets each definition's position.
+std::string user_defs_text(const Module& m, std::map<std::string, int>* index);
+
 // Binds cfg constants to the model (ASSUME of compaction.tla:25-35 included).
+// An INVARIANTS name that is not one of the spec's four as published becomes
+// a user invariant (tlcg_model.user_defs, which then points into static
+// storage of this file: one model bound per process).
 // On failure `err` carries TLC-style text and `exit_code` TLC's exit status.
 // `fairness` (may be null) gets the SPECIFICATION's fairness: TLCG_FAIR_NONE
 // for Spec, TLCG_FAIR_WF_NEXT for a module definition Spec /\ WF_vars(Next).

@@ -70,15 +70,18 @@ std::string prob_str(double p) {  // Java-like "3.8E-11"
 
 void usage() {
   std::fprintf(stderr,
-               "usage: tlc-hip [-config FILE.cfg] [-deadlock] [-workers N] [-gpu D | -gpus N] [-fpbits B]\n"
+               "usage: tlc-hip [-config FILE.cfg] [-deadlock] [-workers N] [-gpu D | -gpus N] [-fpbits B] [-defs FILE]\n"
                "               [-checkpoint MINUTES] [-metadir DIR] [-recover DIR]\n"
                "               [-tlc-order] [-no-trace] [-json] [-dump-defs] [SPEC.tla]\n"
-               "  without SPEC.tla: the built-in compaction module, with -config FILE.cfg\n");
+               "  without SPEC.tla: the built-in compaction module, with -config FILE.cfg\n"
+               "  -defs FILE: definitions added to the built-in module (\"Name == expr\" at column 1), e.g.\n"
+               "              invariants the cfg names (user invariants: include/tlcgpu.h)\n");
 }
 
 struct Opts {
   std::string spec, cfg, metadir, recover;
   bool deadlock_off = false, tlc_order = false, trace = true, json = false, dump_defs = false;
+  std::string defs;  // -defs FILE: definitions added to the built-in module (user invariants)
   int gpu = 0, gpus = 1, fpbits = 0;
   double checkpoint_min = 30.0;  // TLC's default interval; 0 = never
 };
@@ -143,6 +146,7 @@ int main(int argc, char** argv) {
     else if (a == "-no-trace") o.trace = false;
     else if (a == "-json") o.json = true;
     else if (a == "-dump-defs") o.dump_defs = true;
+    else if (a == "-defs") o.defs = next();
     else if (a == "-h" || a == "-help") { usage(); return 0; }
     else if (!a.empty() && a[0] == '-') { std::fprintf(stderr, "Error: unsupported option %s\n", a.c_str()); usage(); return 255; }
     else o.spec = a;
@@ -162,6 +166,28 @@ int main(int argc, char** argv) {
   Module mod;
   if (builtin) {
     mod = builtin_module();
+    if (!o.defs.empty()) {
+      // definitions added to the built-in module (its .tla text is not at
+      // hand, e.g. on a GPU host): "Name == expr" items at column 1
+      std::string extra;
+      if (!read_file(o.defs, &extra)) { std::printf("Error: cannot read %s\n", o.defs.c_str()); return 255; }
+      Module add;
+      if (!parse_module("---- MODULE defs ----\n" + extra + "\n====\n", &add, &err)) {
+        std::printf("Error: %s\n", err.c_str());
+        return 150;
+      }
+      for (Def d : add.defs) {
+        if (d.name == "__DECLARATIONS__" || d.name == "ASSUME") continue;
+        d.line0 -= 1;
+        d.line1 -= 1;
+        auto it = mod.by_name.find(d.name);
+        if (it != mod.by_name.end()) mod.defs[it->second] = d;
+        else {
+          mod.by_name[d.name] = mod.defs.size();
+          mod.defs.push_back(d);
+        }
+      }
+    }
   } else {
     if (!read_file(o.spec, &tla)) { std::printf("Error: cannot read %s\n", o.spec.c_str()); return 255; }
     if (!parse_module(tla, &mod, &err)) { std::printf("Error: %s\n", err.c_str()); return 150; }
@@ -186,9 +212,9 @@ int main(int argc, char** argv) {
   if (builtin) std::printf("Parsing file %s (built-in: the definitions of compaction.tla this build implements)\n", o.spec.c_str());
   else std::printf("Parsing file %s\n", o.spec.c_str());
   if (!recognize_compaction(mod, &err)) { std::printf("Error: %s\n", err.c_str()); return 150; }
-  if (!read_file(o.cfg, &cfgtext)) { std::printf("Error: cannot read configuration file %s\n", o.cfg.c_str()); return 150; }
+  if (!read_file(o.cfg, &cfgtext)) { std::printf("Error: cannot read configuration file %s\n", o.cfg.c_str()); return 151; }
   Config cfg;
-  if (!parse_cfg(cfgtext, &cfg, &err)) { std::printf("Error: %s\n", err.c_str()); return 150; }
+  if (!parse_cfg(cfgtext, &cfg, &err)) { std::printf("Error: %s\n", err.c_str()); return 151; }  // ERROR_CONFIG_PARSE
   std::printf("Semantic processing of module %s\n", mod.name.c_str());
   std::printf("Starting... (%s)\n", now_str().c_str());
   tlcg_model model;
@@ -200,6 +226,10 @@ int main(int argc, char** argv) {
   }
   char cerr[512];
   if (tlcg_check_model(&model, cerr, sizeof cerr) != 0) { std::printf("Error: %s\n", cerr); return 150; }
+  if (model.user_defs && o.gpus > 1) {  // user invariants run on one rank (include/tlcgpu.h)
+    std::fprintf(stderr, "tlc-hip: the cfg has invariants added to the module; checking on one GPU\n");
+    o.gpus = 1;
+  }
   const std::string recover_file = o.recover.empty() ? "" : o.recover + kCheckpointFile;
   if (!recover_file.empty()) {
     std::ifstream probe(recover_file, std::ios::binary);

@@ -65,11 +65,11 @@ def test_numeric_twin_reaches_the_gpu(tmp_path):
     (dict(KeySpace="{0, 1}"), "Assumption line 25, col 8 to line 35, col 35 of module compaction is false.", 10),
     (dict(MessageSentLimit="-1"), "is false.", 10),
     (dict(RetainNullKey="1"), "Evaluating assumption", 75),
-    (dict(MaxCrashTimes=None), "The constant parameter MaxCrashTimes is not assigned a value", 150),
-    (dict(INVARIANTS="TypeSafe, NoSuchInvariant"), "NoSuchInvariant specified in the configuration file is not defined", 150),
-    (dict(INVARIANTS="Termination"), "not one this checker implements", 150),
-    (dict(PROPERTY="TypeSafe"), "temporal property TypeSafe is not one this checker implements", 150),
-    (dict(PROPERTY="NoSuchProperty"), "The property NoSuchProperty specified in the configuration file is not defined", 150),
+    (dict(MaxCrashTimes=None), "The constant parameter MaxCrashTimes is not assigned a value", 151),
+    (dict(INVARIANTS="TypeSafe, NoSuchInvariant"), "NoSuchInvariant specified in the configuration file is not defined", 151),
+    (dict(INVARIANTS="Termination"), "Termination cannot be checked: definition Termination: a temporal formula ([] or <>) is not a state predicate at line 303", 150),
+    (dict(PROPERTY="TypeSafe"), "temporal property TypeSafe is not one this checker implements", 151),
+    (dict(PROPERTY="NoSuchProperty"), "The property NoSuchProperty specified in the configuration file is not defined", 151),
 ])
 def test_cfg_errors(tmp_path, over, expect, code):
     rc, out = run_cli(tmp_path, numeric_cfg(**over))
@@ -138,4 +138,39 @@ def test_fair_specification_is_accepted(tmp_path):
     assert "Computing initial states..." in out
     cfg = numeric_cfg(PROPERTY="Termination").replace("SPECIFICATION Spec", "SPECIFICATION OddSpec")
     rc, out = run_cli(tmp_path, cfg, tla_text=fair_tla)
-    assert "supports SPECIFICATION Spec" in out and rc == 150
+    assert "supports SPECIFICATION Spec" in out and rc == 151
+
+
+@needs_ref
+def test_injected_invariant_is_compiled(tmp_path):
+    """BASELINE config 5: a definition added to compaction.tla and named in
+    INVARIANTS is compiled (user_inv.cpp) and the run goes on to the GPU"""
+    text = open(TLA).read()
+    end = text.rindex("\n====") + 1
+    added = ("LedgerCount ==\n    Cardinality({i \\in 1..CompactionTimesLimit : compactedLedgers[i] # Nil}) <= 2\n\n"
+             "BoundedContext ==\n    /\\ compactedTopicContext \\in 0..CompactionTimesLimit\n"
+             "    /\\ MaxCompactedLedgerId(compactedLedgers) >= compactedTopicContext\n\n")
+    rc, out = run_cli(tmp_path, numeric_cfg(INVARIANTS="TypeSafe, LedgerCount, BoundedContext"),
+                      tla_text=text[:end] + added + text[end:])
+    assert "Computing initial states..." in out
+    assert ("hipSetDevice" in out and rc == 255) or "Invariant LedgerCount is violated." in out
+
+
+@needs_ref
+def test_injected_invariant_outside_the_subset_is_refused(tmp_path):
+    text = open(TLA).read()
+    end = text.rindex("\n====") + 1
+    added = "Weird ==\n    \\A s \\in SUBSET KeySpace : Cardinality(s) <= 2\n\n"
+    rc, out = run_cli(tmp_path, numeric_cfg(INVARIANTS="TypeSafe, Weird"), tla_text=text[:end] + added + text[end:])
+    assert "invariant Weird cannot be checked" in out and "SUBSET" in out and "line" in out
+    assert rc == 150
+
+
+@needs_ref
+def test_edited_spec_invariant_becomes_a_user_invariant(tmp_path):
+    """an edited CompactionHorizonCorrectness is checked from its new text, not refused"""
+    text = open(TLA).read().replace("compactedLedger[j].id >= messagesBeforeHorizon[i].id",
+                                    "compactedLedger[j].id > messagesBeforeHorizon[i].id")
+    assert text != open(TLA).read()
+    rc, out = run_cli(tmp_path, numeric_cfg(), tla_text=text)
+    assert "Computing initial states..." in out

@@ -71,7 +71,7 @@ def header(gpus=1):
     run_line = ("Running breadth-first search Model-Checking with 1 GPU (device 0) and seed 0." if gpus == 1 else
                 f"Running breadth-first search Model-Checking with {gpus} GPU ranks (FPSet partitioned by owner, "
                 f"rank r on device r mod 1) and seed 0.")
-    return ["tlc-hip: TLC-compatible breadth-first model checking on MI355X (libtlcgpu ABI 2)", run_line,
+    return ["tlc-hip: TLC-compatible breadth-first model checking on MI355X (libtlcgpu ABI 3)", run_line,
             "Parsing file compaction.tla (built-in: the definitions of compaction.tla this build implements)",
             "Semantic processing of module compaction", "Starting... (<DATE>)", "Computing initial states..."]
 
@@ -158,3 +158,35 @@ def test_cli_termination_property(tmp_path):
     j = i + 7 + len(first)
     assert lines[i + 8:j] == first[1:] and lines[j:j + 2] == ["", "State 2: Stuttering"]
     assert f"{want['generated']} states generated, {want['distinct']} distinct states found, 0 states left on queue." in lines
+
+
+def test_cli_injected_invariant(tmp_path):
+    """BASELINE config 5: an invariant added to the module (here with -defs, as
+    the box has no .tla) and named in INVARIANTS, violated at depth 12: TLC's
+    -workers 1 trace, its counts where it stops, exit code 12 -- the Python
+    oracle's fixture (tests/golden/user_inv.json, oracle/tla_eval.py)"""
+    import json
+    from user_inv_cases import CASES
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "user_inv.json")))
+    want = g["U_LedgerCount"]["result"]
+    defs = tmp_path / "added.tla"
+    defs.write_text("\\* an invariant the user adds\nLedgerCount == " + CASES["LedgerCount"] + "\n")
+    rc, lines = run(tmp_path, numeric_cfg(INVARIANTS="LedgerCount"), ["-defs", str(defs)])
+    expect = header() + ["Finished computing initial states: 729 distinct states generated at <DATE>.",
+                         "Error: Invariant LedgerCount is violated.",
+                         "Error: The behavior up to this point is:"]
+    for i, t in enumerate(want["trace"]):
+        if t["action"] == "Init":
+            expect.append(f"State {i + 1}: <Initial predicate>")
+        else:
+            l0, c0, l1, c1 = EXTENT[t["action"]]
+            expect.append(f"State {i + 1}: <{t['action']} line {l0}, col {c0} to line {l1}, col {c1} of module "
+                          f"compaction>")
+        expect += t["state"].split("\n") + [""]
+    expect += [f"{want['generated']} states generated, {want['distinct']} distinct states found, "
+               f"{want['left_on_queue']} states left on queue.",
+               f"The depth of the complete state graph search is {want['depth']}.",
+               "Finished in <T> at (<DATE>)"]
+    assert rc == 12
+    assert lines == expect
+    assert len(want["trace"]) == 12
