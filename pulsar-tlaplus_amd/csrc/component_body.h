@@ -13,8 +13,8 @@ namespace tlcg {
 
 // slot of a local key in a T-slot table (multiply-shift, T need not be a power of 2)
 template <int T>
-__device__ __forceinline__ unsigned slot_of(uint32_t key) {
-  return (unsigned)(((unsigned long long)(key * 0x9E3779B1u) * (unsigned)T) >> 32);
+__device__ __forceinline__ unsigned slot_of(uint32_t key, uint32_t mult = 0x9E3779B1u) {
+  return (unsigned)(((unsigned long long)(key * mult) * (unsigned)T) >> 32);
 }
 
 // bucket of a local key in an NB-bucket table (xorshift-multiply, then
@@ -183,7 +183,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     }
     if (act && alive) {
 #ifndef TLCG_BUCKETS
-      H(slot_of<T>(k0)) = 1;
+      H(slot_of<T>(k0, a.mult)) = 1;
 #else
       hb[bucket_of<NB>(k0)][lane] = 1;
 #endif
@@ -348,7 +348,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       else crash = crash_step_k(L, s, &t2) != 0;
       // both successors' first FPSet slots (buckets) are read together
 #ifndef TLCG_BUCKETS
-      const unsigned sl1 = slot_of<T>(t), sl2 = slot_of<T>(t2);
+      const unsigned sl1 = slot_of<T>(t, a.mult), sl2 = slot_of<T>(t2, a.mult);
       const unsigned e1 = H(sl1);  // (unconditional reads; unused when the action is disabled)
       unsigned e2 = H(sl2);
 #else

@@ -136,6 +136,79 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
   return true;
 }
 
+uint32_t tune_slot_mult(const HostModel& hm, int T, int group, int candidates) {
+  const Layout& L = hm.L;
+  const uint32_t def = 0x9E3779B1u;
+  if (L.producer || T <= 0 || group <= 0) return def;
+  // the insert calls of component 0's BFS, in the kernels' order: per depth,
+  // chunks of `group` states; per chunk the compactor successors, then BrokerCrash's
+  const u128 s0 = init_state<u128>(L, 0);
+  const CompMsgs cm = comp_msgs_init(L, (u64)s0);
+  const CodeConsts kc = code_consts(L, cm);
+  std::vector<std::vector<uint32_t>> calls{{code_encode_w<u128>(L, s0)}};
+  {
+    std::unordered_set<uint32_t> seen{calls[0][0]};
+    std::vector<uint32_t> level{calls[0][0]};
+    while (!level.empty() && seen.size() < (size_t)T) {
+      std::vector<uint32_t> next;
+      for (size_t b = 0; b < level.size(); b += (size_t)group) {
+        std::vector<uint32_t> c1, c2;
+        for (size_t i = b; i < b + (size_t)group && i < level.size(); ++i) {
+          ckey t = 0, t2 = 0;
+          int act = 0;
+          if (compactor_step_cb(L, kc, level[i], &t, &act) == 1) c1.push_back(t);
+          if (crash_step_c(L, level[i], &t2)) c2.push_back(t2);
+        }
+        for (auto* c : {&c1, &c2}) {
+          if (c->empty()) continue;
+          calls.push_back(*c);
+          for (uint32_t k : *c)
+            if (seen.insert(k).second) next.push_back(k);
+        }
+      }
+      level.swap(next);
+    }
+    if (seen.size() >= (size_t)T) return def;  // does not fit the table: nothing to tune
+  }
+  auto trips = [&](uint32_t mult) {
+    std::vector<uint32_t> h((size_t)T, 0);
+    long total = 0;
+    for (const auto& c : calls) {
+      int longest = 0;
+      for (uint32_t key : c) {
+        unsigned sl = (unsigned)(((unsigned long long)(key * mult) * (unsigned)T) >> 32);
+        int p = 1;
+        for (; p <= T; ++p) {
+          if (h[sl] == 0) {
+            h[sl] = key + 1;
+            break;
+          }
+          if (h[sl] == key + 1) break;
+          sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
+        }
+        longest = std::max(longest, p);
+      }
+      total += longest;
+    }
+    return total;
+  };
+  uint32_t best = def;
+  long best_t = trips(def);
+  uint64_t x = 0x2545F4914F6CDD1Dull;  // a fixed sequence: the choice is deterministic
+  for (int i = 0; i < candidates; ++i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    const uint32_t m = (uint32_t)(x >> 16) | 1u;
+    const long t = trips(m);
+    if (t < best_t) {
+      best_t = t;
+      best = m;
+    }
+  }
+  return best;
+}
+
 template <typename W>
 std::string format_state(const HostModel& hm, W s) {
   const Layout& L = hm.L;

@@ -28,6 +28,15 @@ bool compile_user_invariants(const tlcg_model& m, const HostModel& hm, const std
                              UserProg* P, std::string* err);
 std::vector<std::string> user_def_names(const char* text);
 
+// The FPSet slot-hash multiplier (multiply-shift over a T-slot table, linear
+// probing) with the fewest probe-loop trips on the insert sequence of the
+// first component's BFS in component codes.  Without a Producer every
+// component has the same code graph (component_code.h), so the choice holds
+// for all of them; the FPSet stays exact for any multiplier.  `group` lanes
+// insert together and wait for the longest probe (1: a lane of the component
+// engine per component; 16: a component of the tree's closed mode).
+uint32_t tune_slot_mult(const HostModel& hm, int T, int group, int candidates);
+
 // every invariant of the cfg, the user's included: -1, else (index << 1) | is_error
 template <typename W>
 int host_check_all(const HostModel& hm, W s) {

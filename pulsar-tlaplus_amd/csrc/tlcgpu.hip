@@ -23,6 +23,7 @@
 #include <sys/mman.h>
 
 #include "component.h"
+#include "component_body.h"  // (CodeShape: the code pass's FPSet size)
 #include "component_code.h"
 #include "tree.h"
 #include "exchange.h"
@@ -778,6 +779,7 @@ struct tlcg_ctx {
   tlcg_opts opts;
   HostModel hm;
   std::string user_defs;                 // model.user_defs points here (tlcg_create copies the caller's text)
+  uint32_t comp_mult = 0, tree_mult = 0;  // tuned slot-hash multipliers (0: not yet)
   UserProg* d_prog = nullptr;            // the user invariants' program on the device (user_inv.h)
   unsigned long long* d_uev = nullptr;   // k_user_check's event (min)
   int words = 1;  // u64 words per state: 1, or 2 for wide layouts (> 63 bits)
@@ -1816,6 +1818,10 @@ int run_component(tlcg_ctx* c) {
   c->jit_used = want_jit && c->jit_state == 1;
   const char* cv = std::getenv("TLCG_CODE");  // 0: 32-bit local keys throughout (A/B)
   c->comp_code = code_bits(L) <= 16 && !(cv && std::atoi(cv) == 0);
+  if (c->comp_code && !c->comp_mult) {
+    const char* tv = std::getenv("TLCG_TUNE_MULT");  // 0: the default multiplier (A/B)
+    c->comp_mult = tv && std::atoi(tv) == 0 ? DEFAULT_SLOT_MULT : tune_slot_mult(c->hm, CodeShape<64>::T, 1, 4096);  // (component_body.h)
+  }
   // on-chip capacity cascade; the first step is tunable (TLCG_COMP_K0 = 32 / 64)
   int kCascade[4] = {64, 128, 255, 0};
   if (const char* k0 = std::getenv("TLCG_COMP_K0"))
@@ -1861,6 +1867,8 @@ int run_component(tlcg_ctx* c) {
     // the first pass runs component codes when they fit 16 bits (component_code.h);
     // a component whose initial key is no code, and the cascade, run 32-bit keys
     const bool code = p == 0 && K <= 64 && c->comp_code;
+    // the code pass's slot hash, tuned on one component (all share its code graph)
+    a.mult = code ? c->comp_mult : DEFAULT_SLOT_MULT;
     if (!(c->jit_used ? jit_launch_component(c->jit, a, K, code, c->stream) : launch_component(a, K, code, c->stream))) {
       c->err = "component kernel launch failed";
       return -1;
@@ -1987,6 +1995,10 @@ int run_tree(tlcg_ctx* c) {
   }
   c->jit_used = want_jit && c->jit_state == 1;
   const int words = c->words;
+  if (closed && !c->tree_mult) {  // (640-slot tables, 16 lanes per component; tree_body.h)
+    const char* tv = std::getenv("TLCG_TUNE_MULT");
+    c->tree_mult = tv && std::atoi(tv) == 0 ? DEFAULT_SLOT_MULT : tune_slot_mult(c->hm, 640, 16, 4096);
+  }
   for (int cap : closed ? std::vector<int>{640, 2048} : std::vector<int>{384, 1024}) {
     const u64 slots = comps * (u64)cap;
     // the store (state words + parent), the depth bytes and the sizes must fit next to what is allocated
@@ -2040,6 +2052,7 @@ int run_tree(tlcg_ctx* c) {
       a.max_n = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV * TREE_STRIPES + 1);
       a.stripe = 2 * TREE_MAXLV;
       a.nstripe = TREE_STRIPES;
+      a.mult = closed ? c->tree_mult : DEFAULT_SLOT_MULT;
       const bool jit = c->jit_used && (cap == 384 || cap == 1024 || cap == 640 || cap == 2048);
       const int g = cap == 384 || cap == 640 ? groups : 1;
       if (!(jit ? jit_launch_tree(c->jit, a, cap, c->stream) : launch_tree(a, cap, g, closed, words, c->stream))) {

@@ -118,8 +118,9 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   auto insert = [&](bool pred, uint32_t key, u64 pref, int dd) {
     bool isnew = false;
     if (pred) {
-      unsigned s = TPOW2 ? (key * (uint32_t)TLCG_TREE_MULT) >> (32 - log2t)
-                         : (unsigned)(((unsigned long long)(key * (uint32_t)TLCG_TREE_MULT) * (unsigned)TT) >> 32);
+      const uint32_t mult = CLOSED ? a.mult : (uint32_t)TLCG_TREE_MULT;
+      unsigned s = TPOW2 ? (key * mult) >> (32 - log2t)
+                         : (unsigned)(((unsigned long long)(key * mult) * (unsigned)TT) >> 32);
       for (int p = 0; p < TT; ++p) {
         const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
         // Producer mode: the probe loop with one exit (P8 2.07 -> 1.99 ms);

@@ -29,8 +29,6 @@ const char* kActionName[] = {"Producer", "CompactorPhaseOne", "CompactorPhaseTwo
                              "CompactorPhaseTwoUpdateContext", "CompactorPhaseTwoUpdateHorizon",
                              "CompactorPhaseTwoPersistCusror", "CompactorPhaseTwoDeleteLedger",
                              "BrokerCrash", "Consumer", "Terminating"};
-const char* kInvName[] = {"TypeSafe", "CompactedLedgerLeak", "CompactionHorizonCorrectness",
-                          "DuplicateNullKeyMessage"};
 
 bool read_file(const std::string& p, std::string* out) {
   std::ifstream f(p, std::ios::binary);
@@ -404,12 +402,12 @@ int main(int argc, char** argv) {
     }
     switch (tst.status) {
       case TLCG_VIOLATION:
-        std::printf("Error: Invariant %s is violated%s.\n", kInvName[model.invariants[tst.invariant]],
+        std::printf("Error: Invariant %s is violated%s.\n", cfg.invariants[(size_t)tst.invariant].c_str(),
                     tst.depth <= 1 && tst.event_gidx == ~0ull ? " by the initial state" : "");
         rc = 12;
         break;
       case TLCG_INVARIANT_ERROR:
-        std::printf("Error: Evaluating invariant %s failed.\n", kInvName[model.invariants[tst.invariant]]);
+        std::printf("Error: Evaluating invariant %s failed.\n", cfg.invariants[(size_t)tst.invariant].c_str());
         rc = 75;
         break;
       case TLCG_DEADLOCK:

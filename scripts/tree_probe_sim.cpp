@@ -52,10 +52,25 @@ int main(int argc, char** argv) {
         if (!pred) continue;
         unsigned s = slot(key);
         int p = 0;
+        if (std::getenv("BUCKET")) {  // 4-slot buckets: one 16-B read shows a bucket; the first empty slot takes the key
+          unsigned b = s / 4;
+          const unsigned nb = (unsigned)TT / 4;
+          for (; p < TT; ++p) {
+            bool done = false;
+            for (int q = 0; q < 4 && !done; ++q) {
+              uint32_t& e = h[b * 4 + q];
+              if (e == key + 1) done = true;
+              else if (e == 0) { e = key + 1; added.push_back(key); done = true; }
+            }
+            if (done) break;
+            b = b + 1 == nb ? 0 : b + 1;
+          }
+        } else {
         for (; p < TT; ++p) {
           if (h[s] == 0) { h[s] = key + 1; added.push_back(key); break; }
           if (h[s] == key + 1) break;
           s = s + 1 == (unsigned)TT ? 0 : s + 1;
+        }
         }
         longest = std::max(longest, p + 1);
         probes += p + 1;
