@@ -69,6 +69,32 @@ def load_profile(name):
     return json.load(open(hits[-1])) | {"_file": os.path.relpath(hits[-1], ROOT)} if hits else None
 
 
+def pmc_fields(name, kernel, kt_s, distinct):
+    """traffic and issue of the dominant kernel from profiles/<newest round>_pmc_<name>.json
+    (scripts/pmc_kernel.sh + scripts/pmc_summarize.py: one complete check per
+    rocprofv3 pass, FETCH_SIZE doubled for gfx950), priced at this run's kernel
+    time kt_s; None when the profile is of another kernel"""
+    pmc = load_profile(f"pmc_{name}.json")
+    if not pmc or "counters" not in pmc or not any(kernel.split()[0].split("<")[0] in k for k in pmc.get("kernels", [])):
+        return None
+    c = pmc["counters"]
+    t_valu = c["SQ_INSTS_VALU"] * 2 / (CUS * SIMDS * CLOCK_HZ)
+    t_salu = c["SQ_INSTS_SALU"] / (CUS * CLOCK_HZ)
+    t_lds = c["SQ_LDS_IDX_ACTIVE"] / (CUS * CLOCK_HZ)
+    return dict(
+        traffic=round(pmc["hbm_bytes"] / kt_s / 1e9, 1),
+        traffic_bytes_per_step=round(pmc["hbm_bytes"]),
+        traffic_source=pmc["_file"],
+        issue=dict(frac=round(max(t_valu, t_salu, t_lds) / kt_s, 3),
+                   valu_ms=round(t_valu * 1e3, 3), salu_ms=round(t_salu * 1e3, 3), lds_ms=round(t_lds * 1e3, 3),
+                   valu_wave_insts_per_state=round(c["SQ_INSTS_VALU"] / distinct, 3),
+                   salu_wave_insts_per_state=round(c["SQ_INSTS_SALU"] / distinct, 3),
+                   wave_issue_frac=round(c["SQ_ACTIVE_INST_ANY"] / max(c["SQ_WAVE_CYCLES"], 1), 3),
+                   lds_bank_conflict_frac=round(c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_LDS_IDX_ACTIVE"], 1), 3),
+                   formula="frac = max(VALU x 2 cyc / (256 CU x 4 SIMD), SALU x 1 cyc / 256 CU, "
+                           "SQ_LDS_IDX_ACTIVE / 256 CU) / 2.4 GHz / kernel time (DESIGN 4)"))
+
+
 def load_microbench(rel):
     """Best measured rate per access kind (accesses/s) from the microbenchmark log."""
     p = os.path.join(ROOT, rel)
@@ -286,6 +312,11 @@ def main():
         eng.close()
         if (r.generated, r.distinct, r.depth) != (cfg["generated"], cfg["distinct"], cfg["depth"]):
             raise SystemExit(f"count mismatch (exchange): {(r.generated, r.distinct, r.depth)} want {cfg}")
+        if r.engine == "tree":  # Producer modelled: each rank ran whole subtrees of the component tree
+            return dict(engine="tree", jit=1, elapsed=float(t[0]), expand_ms=float(t[1]) / args.steps,
+                        kernel_ms=float(t[2]) / args.steps, launches=cfg.get("N", 3) + 1,
+                        partition="component tree, whole subtrees per rank (csrc/tree.h): no exchange",
+                        exchange="none on the data path: tlcg_run_comm all-reduces the combined counts over RCCL")
         return dict(engine="global", jit=0, elapsed=float(t[0]), expand_ms=float(t[1]) / args.steps,
                     kernel_ms=float(t[2]) / args.steps, launches=cfg["depth"] - 1,
                     kernel="k_expand<u64, open partition> + k_absorb",
@@ -297,7 +328,8 @@ def main():
     exchange_run = global_run = None
     exchange_error = None
     if open_model and distributed:
-        main_run = time_exchange(0)  # successors leave their rank: the exchange is the path
+        # the component tree split by subtrees (no exchange), or the level loop's exchange if it hands over
+        main_run = time_exchange(0)
     else:
         main_run = time_engine("auto")
         global_run = time_engine("global")  # the HBM-FPSet engine beside the on-chip one
@@ -338,7 +370,12 @@ def main():
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
                   bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
                   kernel_bytes_per_distinct=round(abytes / distinct, 2))
-        pmc = load_profile(PMC_PROFILE)
+        new = pmc_fields(f"expand_{args.config}", rf["kernel"], r["expand_ms"] * 1e-3, distinct) \
+            if world == 1 and words == 1 and not open_model else None
+        if new:
+            rf.update(new)
+            rf["traffic_over_algorithmic"] = round(new["traffic_bytes_per_step"] / abytes, 2)
+        pmc = None if new else load_profile(PMC_PROFILE)
         avg_launch_s = r["expand_ms"] / r["launches"] * 1e-3
         if pmc and args.config == "g9" and world == 1 and words == 1 and not open_model:
             rf["traffic"] = round(pmc["hbm_bytes_per_launch"] / avg_launch_s / 1e9, 1)
@@ -369,6 +406,11 @@ def main():
                   bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
                   kernel_bytes_per_distinct=COMPONENT_BYTES_PER_STATE,
                   kernel_written_gbs=round(written, 1))
+        kt = r["expand_ms"] * 1e-3
+        new = pmc_fields(f"component_{args.config}", rf["kernel"], kt, distinct) if world == 1 else None
+        if new:
+            rf.update(new)
+            return rf
         pmc = load_profile(PMC_COMPONENT_PROFILE)
         # (the counters are of one kernel variant: used only for that variant)
         if pmc and args.config == "g9" and world == 1 and pmc["kernel"].split()[0] == rf["kernel"].split()[0]:
@@ -408,11 +450,15 @@ def main():
         else:
             kern = ("tlcg_treec_640 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<640, 1024, 4, closed> (") + \
                 "component tree closed mode: component codes, 4 components per wavefront)"
-        return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kern,
-                    launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                    bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, kernel_bytes_per_distinct=per_state,
-                    kernel_written_gbs=round(per_state * distinct / world / (r["expand_ms"] * 1e-3) / 1e9, 1))
+        rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kern,
+                  launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
+                  bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, kernel_bytes_per_distinct=per_state,
+                  kernel_written_gbs=round(per_state * distinct / world / (r["expand_ms"] * 1e-3) / 1e9, 1))
+        new = pmc_fields(f"tree_{args.config}", kern, r["expand_ms"] * 1e-3, distinct) if world == 1 else None
+        if new:
+            rf.update(new)
+        return rf
 
     def summary(r):
         out = dict(engine=r["engine"], jit=bool(r["jit"]), value=round(distinct * args.steps / r["elapsed"], 1),

@@ -106,7 +106,7 @@ class RcclTransport : public Transport {
   int world() const override { return s_->world; }
 
   bool allgather_rows(const uint64_t* row, uint64_t* out, std::string* err) override {
-    const size_t w = (size_t)s_->world + 1;
+    const size_t w = row_width(s_->world);
     hipSetDevice(s_->device);  // (the scratch lives on the rank's device)
     if (!scratch(w + w * (size_t)s_->world, err)) return false;
     std::memcpy(s_->h, row, w * 8);
@@ -152,7 +152,10 @@ class RcclTransport : public Transport {
       }
       off += recv[r];
     }
-    return nccl(R()->GroupEnd(), "ncclGroupEnd", err);  // the absorb that follows is ordered on the stream
+    // the absorb that follows is ordered on the stream; waiting here puts the
+    // records under TLCG_COMM_TIMEOUT_S too (a peer that died mid-exchange
+    // aborts the communicator instead of hanging the absorb)
+    return nccl(R()->GroupEnd(), "ncclGroupEnd", err) && wait(err);
   }
 
   bool allreduce(uint64_t* v, int n, RedOp op, std::string* err) override {
@@ -217,7 +220,10 @@ class RcclTransport : public Transport {
         s_->comm = nullptr;
         return false;
       }
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      // a collective of a few words completes in microseconds: yield while
+      // it is young, back off to 20 us sleeps only past 200 us
+      if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200)) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
   CommState* s_;
@@ -342,7 +348,7 @@ class LocalTransport : public Transport {
   int world() const override { return b_->n; }
 
   bool allgather_rows(const uint64_t* row, uint64_t* out, std::string*) override {
-    const size_t w = (size_t)b_->n + 1;
+    const size_t w = row_width(b_->n);
     std::memcpy(&b_->rows[(size_t)r_ * w], row, w * 8);
     b_->barrier();
     std::memcpy(out, b_->rows.data(), w * (size_t)b_->n * 8);
@@ -406,7 +412,7 @@ LocalBoard* local_board_new(tlcg_ctx* const* ctxs, int n) {
   auto* b = new LocalBoard();
   b->n = n;
   b->ctxs.assign(ctxs, ctxs + n);
-  b->rows.assign((size_t)n * (size_t)(n + 1), 0);
+  b->rows.assign((size_t)n * row_width(n), 0);
   b->red.resize((size_t)n);
   for (int r = 0; r < n; ++r) b->ts.emplace_back(new LocalTransport(b, r));
   return b;
@@ -418,7 +424,8 @@ Transport* local_transport(LocalBoard* b, int rank) { return b->ts[(size_t)rank]
 
 int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* levels, std::string* err) {
   const int n = t.world(), me = t.rank();
-  const size_t w = (size_t)n + 1;
+  // a rank's row: its record count per destination, its failure flag, its inbox capacity
+  const size_t w = row_width(n);
   bool failed = false;
   std::string local_err;
   auto fail_local = [&](const char* what) {
@@ -442,8 +449,19 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
     if (tlcg_run(c, &s) != 0) fail_local("tlcg_run");
   } else {
     if (tlcg_init(c, &s) != 0) fail_local("tlcg_init");
+    // Producer modelled: tlcg_init ran this rank's subtrees of the component
+    // tree to the end (tree.h, no exchange) unless one raised an error to
+    // report or did not fit; then every rank redoes the model on the global
+    // engine with the exchange below, which reports TLC's first error
+    uint64_t tree[2] = {!failed && ctx_engine(c) == TLCG_ENGINE_TREE ? 1u : 0u, failed ? 1u : 0u};
+    if (!t.allreduce(tree, 2, RED_SUM, err)) return -20;
+    const bool all_tree = !tree[1] && tree[0] == (uint64_t)n;
+    if (!all_tree && !failed && ctx_engine(c) == TLCG_ENGINE_TREE) {
+      ctx_disable_tree(c);
+      if (tlcg_init(c, &s) != 0) fail_local("tlcg_init");
+    }
     std::vector<uint64_t> row(w), rows(w * (size_t)n), send((size_t)n), recv((size_t)n);
-    for (;;) {
+    for (; !all_tree;) {
       auto tp = clk();
       // termination (every rank's newest level empty, or an error anywhere),
       // and every local failure since the last collective
@@ -460,22 +478,30 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
         row[(size_t)d] = send[(size_t)d] = k;
       }
       row[(size_t)n] = failed ? 1 : 0;
+      row[(size_t)n + 1] = ctx_inbox_cap(c);
       if (!t.allgather_rows(row.data(), rows.data(), err)) return -20;
       tick(2, tp);
-      bool any = false;
+      bool any = false, grow = false;
       for (int q = 0; q < n; ++q) {
         any |= rows[(size_t)q * w + (size_t)n] != 0;
         recv[(size_t)q] = q == me ? 0 : rows[(size_t)q * w + (size_t)me];
+        uint64_t into_q = 0;  // what rank q receives, against its inbox
+        for (int p = 0; p < n; ++p)
+          if (p != q) into_q += rows[(size_t)p * w + (size_t)q];
+        grow |= into_q > rows[(size_t)q * w + (size_t)n + 1];
       }
       if (any) break;
-      // the inbox is sized on every rank before any record moves
       uint64_t total = 0;
       for (uint64_t x : recv) total += x;
-      if (tlcg_inbox(c, total, nullptr) != 0) fail_local("tlcg_inbox");
-      uint64_t bad = failed ? 1 : 0;
-      if (!t.allreduce(&bad, 1, RED_SUM, err)) return -20;
+      if (grow) {
+        // an inbox must grow before any record moves: every rank learns
+        // whether the allocations held (the rows told all of them to wait)
+        if (tlcg_inbox(c, total, nullptr) != 0) fail_local("tlcg_inbox");
+        uint64_t bad = failed ? 1 : 0;
+        if (!t.allreduce(&bad, 1, RED_SUM, err)) return -20;
+        if (bad) break;
+      }
       tick(3, tp);
-      if (bad) break;
       std::string rerr;
       const bool moved = t.records(c, send.data(), recv.data(), &rerr);
       tick(4, tp);

@@ -24,13 +24,18 @@ namespace tlcg {
 
 enum RedOp { RED_SUM = 0, RED_MIN = 1, RED_MAX = 2 };
 
+// words of a rank's row in the per-level all-gather: its record count per
+// destination, its failure flag, its inbox capacity (run_ranks)
+inline size_t row_width(int world) { return (size_t)world + 2; }
+
 class Transport {
  public:
   virtual ~Transport() = default;
   virtual int rank() const = 0;
   virtual int world() const = 0;
   // row[d] = records this rank holds for rank d (row[rank] = 0), row[world] =
-  // this rank's failure flag; out gets every rank's row (world x (world + 1))
+  // this rank's failure flag, row[world + 1] its inbox capacity; out gets
+  // every rank's row (world x row_width(world))
   virtual bool allgather_rows(const uint64_t* row, uint64_t* out, std::string* err) = 0;
   // every outbox of ctx to its owner; the inbox (already sized for the sum of
   // recv) receives them source-rank-major.  Ordered before later work on the
@@ -54,6 +59,9 @@ void comm_free(void* comm_state);
 
 // context internals exchange.cpp needs (tlcgpu.hip)
 int ctx_device(const tlcg_ctx* c);
+int ctx_engine(const tlcg_ctx* c);         // TLCG_ENGINE_* of the last tlcg_init
+uint64_t ctx_inbox_cap(const tlcg_ctx* c); // records the inbox holds without growing
+void ctx_disable_tree(tlcg_ctx* c);        // the next tlcg_init runs the global engine
 void ctx_rank_world(const tlcg_ctx* c, int* rank, int* world);
 void*& ctx_comm(tlcg_ctx* c);
 void ctx_set_error(tlcg_ctx* c, const std::string& e);

@@ -620,6 +620,13 @@ int run_liveness(const HostModel& hm, const tlcg_opts* o, int fair, tlcg_livenes
     if (!mem.alloc(&B.slots, nslots * (sizeof(W) / 8)) || !mem.alloc(&B.store, cap) || !mem.alloc(&B.parent, cap) ||
         !mem.alloc(&B.slot_of, cap) || !mem.alloc(&B.gidx_of, nslots) || !mem.alloc(&B.indeg, nslots) ||
         !mem.alloc(&B.stuck, cap) || !mem.alloc(&B.ctr, 1)) {
+      if (cap > (1ull << 20) && attempt < 8) {
+        // what HBM holds beside the caller's other buffers: a smaller start,
+        // grown x4 below only if G' needs it
+        cap /= 2;
+        log2 = 0;
+        continue;
+      }
       *err = "liveness: device allocation failed (" + std::to_string(cap) + " states, 2^" + std::to_string(lg) +
              " FPSet slots)";
       return -5;

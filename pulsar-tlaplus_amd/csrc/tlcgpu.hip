@@ -780,6 +780,7 @@ struct tlcg_ctx {
   HostModel hm;
   std::string user_defs;                 // model.user_defs points here (tlcg_create copies the caller's text)
   uint32_t comp_mult = 0, tree_mult = 0;  // tuned slot-hash multipliers (0: not yet)
+  bool no_tree = false;                   // the ranks fell back from the sharded component tree (run_ranks)
   UserProg* d_prog = nullptr;            // the user invariants' program on the device (user_inv.h)
   unsigned long long* d_uev = nullptr;   // k_user_check's event (min)
   int words = 1;  // u64 words per state: 1, or 2 for wide layouts (> 63 bits)
@@ -911,6 +912,9 @@ struct tlcg_ctx {
 
 namespace tlcg {
 int ctx_device(const tlcg_ctx* c) { return c->opts.device; }
+int ctx_engine(const tlcg_ctx* c) { return c->engine; }
+uint64_t ctx_inbox_cap(const tlcg_ctx* c) { return c->inbox_cap; }
+void ctx_disable_tree(tlcg_ctx* c) { c->no_tree = true; }
 void ctx_rank_world(const tlcg_ctx* c, int* rank, int* world) {
   *rank = c->opts.rank;
   *world = c->opts.world;
@@ -1933,7 +1937,7 @@ bool tree_applicable(const tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   const int mb = L.msg_sh + L.N * L.mw;
   const char* tv = std::getenv("TLCG_TREE");
-  return L.producer && !(tv && std::atoi(tv) == 0) && !c->opts.tlc_order && c->opts.world == 1 && c->words == 1 &&
+  return L.producer && !(tv && std::atoi(tv) == 0) && !c->no_tree && !c->opts.tlc_order && c->words == 1 &&
          L.bits - mb <= 31 && L.N >= 1 && L.N <= 8 && !c->opts.outdegree && L.nkv >= 1 && c->hm.n_init >= 1 &&
          !c->opts.device_store_cap && !c->opts.fpset_spill && !c->hm.user;
 }
@@ -1961,16 +1965,41 @@ int run_tree(tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   const bool closed = !L.producer;
   std::vector<u64> ncomp;  // components per launch (layer): nkv^l, or this rank's initial states
+  std::vector<u64> lbase;  // the layer's number of the launch's component 0
   u64 r0 = 0;
+  const u64 W = (u64)c->opts.world, R = (u64)c->opts.rank;
+  int shard = 0;  // Producer, W > 1: the layer whose components are split between the ranks
   if (closed) {
-    const u64 W = (u64)c->opts.world, R = (u64)c->opts.rank;
     r0 = c->hm.n_init * R / W;
     ncomp.push_back(c->hm.n_init * (R + 1) / W - r0);
+    lbase.push_back(0);
   } else {
-    ncomp.push_back(1);
-    for (int l = 1; l <= L.N; ++l) {
-      if (ncomp.back() > (1ull << 34) / (u64)L.nkv) return 0;
-      ncomp.push_back(ncomp.back() * (u64)L.nkv);
+    // every component of layer l >= 1 lies in the subtree of one component of
+    // layer `shard` (its first `shard` messages; compaction.tla:83-87 only
+    // appends), so the ranks split layer `shard` into contiguous ranges and
+    // each runs its subtrees alone -- no exchange.  The layers above it (a
+    // few components) run on every rank and count on rank 0.
+    u64 width = 1;
+    if (W > 1)
+      while (shard < L.N && width < W) {
+        width *= (u64)L.nkv;
+        ++shard;
+      }
+    const u64 a = width * R / W, b = width * (R + 1) / W;
+    u64 full = 1;  // nkv^l
+    for (int l = 0; l <= L.N; ++l) {
+      if (l) {
+        if (full > (1ull << 34) / (u64)L.nkv) return 0;
+        full *= (u64)L.nkv;
+      }
+      if (W == 1 || l < shard) {
+        ncomp.push_back(full);
+        lbase.push_back(0);
+      } else {
+        const u64 per = full / width;  // nkv^(l - shard)
+        ncomp.push_back((b - a) * per);
+        lbase.push_back(a * per);
+      }
     }
   }
   u64 comps = 0;
@@ -2036,6 +2065,9 @@ int run_tree(tlcg_ctx* c) {
       a.n_comp = ncomp[l];
       a.n_init = c->hm.n_init;
       a.comp0 = r0;
+      a.comp_base = lbase[l];
+      a.par_comp_base = l ? lbase[l - 1] : 0;
+      a.count = closed || W == 1 || (int)l >= shard || R == 0;
       a.par_states = l ? c->d_states + pgbase : nullptr;
       a.par_dep = l ? c->d_tree_dep + pgbase : nullptr;
       a.par_n = l ? c->d_tree_n + pcbase : nullptr;
@@ -2099,7 +2131,7 @@ int run_tree(tlcg_ctx* c) {
     c->comp_levels.assign(c->h_tree_ctr, c->h_tree_ctr + TREE_MAXLV);
     c->comp_level_gen.assign(c->h_tree_ctr + TREE_MAXLV, c->h_tree_ctr + 2 * TREE_MAXLV);
     while (!c->comp_levels.empty() && c->comp_levels.back() == 0) c->comp_levels.pop_back();
-    c->comp_init = closed ? ncomp[0] : c->hm.n_init;
+    c->comp_init = closed ? ncomp[0] : R == 0 ? c->hm.n_init : 0;  // (Init counts once, on rank 0)
     c->comp_distinct = 0;
     for (u64 x : c->comp_levels) c->comp_distinct += x;
     c->comp_generated = c->comp_init;
@@ -3217,6 +3249,11 @@ int tlcg_owner(tlcg_ctx* c, uint64_t state) {
 int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
   const DeviceGuard dg(c);
   if (!c || !c->inited) return -1;
+  if (c->engine != TLCG_ENGINE_GLOBAL) {
+    c->err = "the on-chip engine completed this rank's share in tlcg_init: there is no level to expand "
+             "(tlcg_opts.engine = TLCG_ENGINE_GLOBAL for the exchange)";
+    return -2;
+  }
   if (c->status != TLCG_RUNNING) {
     fill_stats(c, st);
     return 0;

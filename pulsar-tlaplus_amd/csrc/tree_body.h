@@ -192,8 +192,9 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
           pc = 0;
           j = 0;
         } else {
-          pc = ci / (u64)L.nkv;
-          j = (int)(ci % (u64)L.nkv);
+          const u64 cg = a.comp_base + ci;  // (the layer's component number)
+          pc = cg / (u64)L.nkv - a.par_comp_base;
+          j = (int)(cg % (u64)L.nkv);
           np = a.par_n[pc];
         }
         pst = a.layer ? a.par_states + pc * CAP : nullptr;
@@ -296,7 +297,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     // the group's sum of generated successors, added by its first lane
 #pragma unroll
     for (int off = S / 2; off > 0; off >>= 1) gen += __shfl_xor(gen, off);
-    if (have && sub == 0 && d < TREE_MAXLV) {
+    if (have && sub == 0 && d < TREE_MAXLV && a.count) {
       atomicAdd(&lvl_d[d], (lvl_t)(f1 - f0));
       atomicAdd(&lvl_g[d], (lvl_t)gen);
     }

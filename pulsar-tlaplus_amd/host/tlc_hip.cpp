@@ -324,8 +324,11 @@ int main(int argc, char** argv) {
     lo.state_capacity = st.distinct;  // G' is a subset of the reachable states
     lo.log2_fpset_slots = 0;
     char lerr[512] = {0};
-    // (the check allocates its own device buffers, about 64 B per not-P state,
-    // beside the safety run's, which the outdegree statistics below still read)
+    // (the check allocates its own device buffers beside the safety run's,
+    // which the outdegree statistics below still read: per state of capacity
+    // the store, parent, slot index and stuck flag, 21-29 B, and 2 FPSet slots
+    // of 20-28 B each -- 60-85 B; it halves the capacity until they fit and
+    // grows it x4 only if G' needs more, liveness.hip)
     if (tlcg_check_termination(&model, &lo, fairness, &lv, lstates.data(), lacts.data(), (int32_t)lacts.size(), &ln,
                                lerr, (int32_t)sizeof lerr) != 0) {
       std::printf("Error: the liveness check failed: %s\n", lerr);

@@ -45,16 +45,25 @@ class DistResult:
     closed: bool
     invariant: Optional[int] = None         # index into the model's invariants (first error)
     first_error_rank: Optional[int] = None
+    engine: str = ""                         # "tree": the ranks ran shares of the component tree
 
 
 class GpuEngine:
     """One rank's libtlcgpu context (the partitioned C-ABI)."""
 
     def __init__(self, model: tlcgpu.Model, rank: int, world: int, device: int, **opts):
+        self.model, self.opts = model, dict(opts)
         self.ck = tlcgpu.Checker(model, device=device, rank=rank, world=world, **opts)
         self.lib, self.ctx, self.stats = self.ck.lib, self.ck.ctx, self.ck.stats
         self.world, self.rank, self.device = world, rank, device
         self.closed = world == 1 or (not model.model_producer and opts.get("partition", 0) in (0, 1))
+
+    def reopen_global(self):
+        """a new context on the global engine (the ranks left the component tree)"""
+        self.ck.close()
+        self.ck = tlcgpu.Checker(self.model, device=self.device, rank=self.rank, world=self.world,
+                                 **dict(self.opts, engine="global"))
+        self.lib, self.ctx, self.stats = self.ck.lib, self.ck.ctx, self.ck.stats
 
     def run_closed(self) -> tlcgpu.tlcg_stats:
         return self.ck.run_raw()
@@ -184,7 +193,8 @@ def run_native(engine: "GpuEngine") -> DistResult:
     levels = [lv[i] for i in range(n.value)]
     return DistResult(status=tlcgpu.STATUS[st.status], generated=st.generated, distinct=st.distinct, depth=st.depth,
                       levels=levels, kernel_ms=st.kernel_ms, expand_ms=st.expand_ms, closed=engine.closed,
-                      invariant=st.invariant if st.invariant >= 0 else None)
+                      invariant=st.invariant if st.invariant >= 0 else None,
+                      engine=tlcgpu.ENGINE_NAMES.get(int(st.engine), "?"))
 
 
 def _transport_device(group, dev: torch.device) -> torch.device:
@@ -206,6 +216,19 @@ def run(engine, group=None, dev: Optional[torch.device] = None, timing: Optional
         return _reduce_result(engine, stats, group, dev)
     xdev = _transport_device(group, dev)
     stats = engine.init()
+    # Producer modelled: each rank ran its subtrees of the component tree in
+    # init (csrc/tree.h, no exchange) -- unless one of them handed the model
+    # to the global engine (an error to report); then every rank does
+    if hasattr(engine, "reopen_global"):
+        tree = torch.tensor([1 if int(stats.engine) == 3 else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(tree, op=dist.ReduceOp.SUM, group=group)
+        if int(tree.item()) == world:
+            r = _reduce_result(engine, stats, group, dev)
+            r.engine = "tree"
+            return r
+        if int(stats.engine) == 3:
+            engine.reopen_global()
+            stats = engine.init()
     me = dist.get_rank(group)
     lv0 = engine.level_sizes()
     flags = torch.tensor([lv0[-1] if lv0 else 0, 1 if stats.status >= 2 else 0], dtype=torch.int64, device=dev)

@@ -13,6 +13,10 @@ pytestmark = pytest.mark.gpu
 
 
 def run_virtual(model, world, partition=0, **opts):
+    # (the exchange API itself: an open partition runs the global engine, not
+    # the component tree's sharded subtrees that tlcg_init would otherwise run)
+    if model.model_producer or partition == 2:
+        opts.setdefault("engine", "global")
     engines = [tdist.GpuEngine(model, r, world, 0, partition=partition, **opts) for r in range(world)]
     try:
         if engines[0].closed:

@@ -158,3 +158,60 @@ def test_tree_random_producer_cfgs(seed):
         assert r.engine == "global", seed
         if want["result"] in ("invariant", "invariant_error"):
             assert r.invariant == want["invariant"], seed
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 8])
+def test_tree_sharded_over_ranks(ranks):
+    """with the Producer modelled, `ranks` contexts (tlcg_run_node,
+    threads on this one GPU) each run whole subtrees of the component tree --
+    the layer that first has >= `ranks` components is split into contiguous
+    ranges, the layers above it run everywhere and count once -- with no
+    exchange; the combined counts and every level are the golden ones"""
+    for case in OK_CASES:
+        m = model_of(GOLDEN[case]["constants"])
+        if tlcgpu.state_words(m) != 1:
+            continue
+        want = GOLDEN[case]["result"]
+        r = tlcgpu.run_node(m, ranks)
+        assert r.engine == "tree", case
+        assert (r.status, r.generated, r.distinct, r.depth) == ("ok", want["generated"], want["distinct"],
+                                                                 want["depth"]), case
+        assert r.levels == want["levels"], case
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "p8.json")))
+    r = tlcgpu.run_node(model_of(g["constants"]), ranks)
+    want = g["result"]
+    assert r.engine == "tree"
+    assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                             want["levels"])
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_tree_sharded_random_producer_cfgs(seed):
+    """seeded random producer cfgs at 2 and 5 ranks against the C oracle run
+    live: counts and levels when the check passes; on an error the ranks hand
+    the model to the global engine's exchange, which reports TLC's verdict"""
+    from conftest import run_oracle
+    m = random_producer_model(seed)
+    if tlcgpu.check_model(m) is not None:
+        pytest.skip(f"constants refused: {tlcgpu.check_model(m)}")
+    want = run_oracle(m)
+    for ranks in (2, 5):
+        r = tlcgpu.run_node(m, ranks)
+        assert r.status == want["result"], (seed, ranks, r.status)
+        assert r.depth == want["depth"], (seed, ranks)
+        if want["result"] == "ok":
+            assert (r.generated, r.distinct, r.levels) == (want["generated"], want["distinct"], want["levels"])
+            assert r.engine == ("tree" if tree_applies(m) else "global"), (seed, r.engine)
+        else:
+            assert r.engine == "global"
+            assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"]), (seed, ranks)
+
+
+@pytest.mark.parametrize("case", ERR_CASES)
+def test_tree_sharded_error_hands_over_to_the_exchange(case):
+    m = model_of(GOLDEN[case]["constants"])
+    want = GOLDEN[case]["result"]
+    r = tlcgpu.run_node(m, 3)
+    assert r.engine == "global"
+    assert r.status == want["result"] and r.depth == want["depth"]
+    assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
