@@ -781,6 +781,8 @@ struct tlcg_ctx {
   std::string user_defs;                 // model.user_defs points here (tlcg_create copies the caller's text)
   uint32_t comp_mult = 0, tree_mult = 0;  // tuned slot-hash multipliers (0: not yet)
   bool no_tree = false;                   // the ranks fell back from the sharded component tree (run_ranks)
+  bool tree_codes = false;                // the store holds the tree's closed-mode component codes (tree_body.h)
+  u64 tree_r0 = 0;                        //   of the components of initial states tree_r0, tree_r0 + 1, ..
   UserProg* d_prog = nullptr;            // the user invariants' program on the device (user_inv.h)
   unsigned long long* d_uev = nullptr;   // k_user_check's event (min)
   int words = 1;  // u64 words per state: 1, or 2 for wide layouts (> 63 bits)
@@ -1619,7 +1621,23 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   st->levels_redone = c->levels_redone;
 }
 
+// the state word of store slot g holding a component code (the tree's closed
+// mode): chunk g / cap is the component of initial state tree_r0 + g / cap
+u128 tree_code_word(const tlcg_ctx* c, u64 g, uint32_t code) {
+  const Layout& L = c->hm.L;
+  const u128 s0 = init_state<u128>(L, c->tree_r0 + g / (u64)c->tree_cap);
+  const CodeConsts kc = code_consts(L, comp_msgs_init(L, (u64)s0));
+  return code_word<u128>(L, kc, s0 & messages_mask<u128>(L), code);
+}
+
 bool state_at(tlcg_ctx* c, u64 g, u128* s, u64* p) {
+  if (c->tree_codes) {
+    uint32_t code = 0;
+    HIPCHK(hipMemcpy(&code, reinterpret_cast<const uint32_t*>(c->d_states) + g, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(p, dev_parent(c, g), 8, hipMemcpyDeviceToHost));
+    *s = tree_code_word(c, g, code);
+    return true;
+  }
   uint64_t w[2] = {0, 0};
   if (g < c->win) {
     const auto& h = chunk_of(c, g);
@@ -2110,6 +2128,10 @@ int run_tree(tlcg_ctx* c) {
     if (flags & TREE_EVENT) return 0;  // the global engine finds TLC's first error and its trace
     if (flags & TREE_OVERFLOW) continue;
     c->tree_cap = cap;
+    // (the closed mode's store holds codes unless an A/B build asked for words)
+    const char* jd = std::getenv("TLCG_JIT_DEFINES");
+    c->tree_codes = closed && !(jd && std::strstr(jd, "TLCG_TREE_CODE_STORE=0"));
+    c->tree_r0 = r0;
     if (std::getenv("TLCG_TREE_STATS")) {  // diagnostics: component sizes per layer
       std::vector<uint32_t> nn(comps);
       HIPCHK_I(hipMemcpy(nn.data(), c->d_tree_n, comps * 4, hipMemcpyDeviceToHost));
@@ -2598,6 +2620,7 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
   if (!c || !c->stream) return -1;
   free_tier(c);
   free_host_chunks(c);
+  c->tree_codes = false;
   c->kernel_ms = c->expand_ms = 0;
   c->status = TLCG_RUNNING;
   c->ev_word = NO_EVENT;
@@ -2709,6 +2732,16 @@ int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* ou
   const DeviceGuard dg(c);
   if (!c || first + n > store_end(c)) return -1;
   const u64 w = c->words;
+  if (c->tree_codes) {  // component codes: decoded here
+    std::vector<uint32_t> codes(n);
+    if (n && hipMemcpy(codes.data(), reinterpret_cast<const uint32_t*>(c->d_states) + first, n * 4,
+                       hipMemcpyDeviceToHost) != hipSuccess) {
+      c->err = "copy failed";
+      return -10;
+    }
+    for (u64 i = 0; i < n; ++i) split_words(tree_code_word(c, first + i, codes[i]), out + i * w, (int)w);
+    return 0;
+  }
   while (n && first < c->win) {  // spilled states
     const auto& h = chunk_of(c, first);
     const u64 m = std::min<u64>(n, h.g0 + h.n - first);

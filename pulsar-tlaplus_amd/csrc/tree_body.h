@@ -27,6 +27,14 @@ namespace tlcg {
 // fewer, so one component per 64-lane wavefront leaves most lanes idle and
 // pays the scalar (exec-mask, loop) instructions once per state; G groups
 // share them.
+// closed mode: the store holds each state's component code (4 B; the host
+// decodes it with the component's messages, tlcg_state_at / copy_states)
+// instead of the state word built from it -- G9-deep: the 93-bit words cost
+// 21 % of the kernel (TLCG_TREE_NO_STORE, profiles/r03_tree_closed_variants.jsonl).
+// 0: words, for A/B
+#ifndef TLCG_TREE_CODE_STORE
+#define TLCG_TREE_CODE_STORE 1
+#endif
 #ifndef TLCG_TREE_MULT  // the slot hash's multiplier (multiply-shift)
 #define TLCG_TREE_MULT 0x9E3779B1u
 #endif
@@ -109,6 +117,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   const uint8_t* pdep = nullptr;
   u64 pgb = 0, gb = 0;
   W* st = nullptr;
+  uint32_t* stc = nullptr;  // (closed mode, TLCG_TREE_CODE_STORE: the chunk as codes)
   u64* par = nullptr;
   uint8_t* dp = nullptr;
   uint32_t* hh = &h[g][0];
@@ -162,7 +171,8 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       par[pos] = pref == NO_PARENT ? NO_PARENT : (a.rank_tag | pref);
       if constexpr (CLOSED) {
 #ifndef TLCG_TREE_NO_STORE  // (experiment only: what the state words cost)
-        st[pos] = code_word<W>(L, kc, msgs, key);
+        if constexpr (TLCG_TREE_CODE_STORE) stc[pos] = key;
+        else st[pos] = code_word<W>(L, kc, msgs, key);
 #endif
 #ifndef TLCG_TREE_NO_INV  // (experiment only: what the invariants cost)
         if (check_invariants_cb(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
@@ -207,6 +217,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         dp = a.dep + ci * CAP;
       }
       st = reinterpret_cast<W*>(a.states) + ci * CAP;
+      stc = reinterpret_cast<uint32_t*>(a.states) + ci * CAP;
       par = a.parents + ci * CAP;
       gb = a.gbase + ci * CAP;
       n = f0 = d = 0;
@@ -264,11 +275,11 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       if constexpr (FB > 0) {
         if (ok && i - f0 < FB) k = fbuf[g][d & 1][i - f0];
         else if (ok) {
-          if constexpr (CLOSED) k = code_encode_w<W>(L, st[i]);
+          if constexpr (CLOSED) k = TLCG_TREE_CODE_STORE ? stc[i] : code_encode_w<W>(L, st[i]);
           else k = (uint32_t)((u64)st[i] >> mb);
         }
       } else if constexpr (CLOSED && KCAP != CAP) {
-        if (ok) k = code_encode_w<W>(L, st[i]);
+        if (ok) k = TLCG_TREE_CODE_STORE ? stc[i] : code_encode_w<W>(L, st[i]);
       } else if constexpr (KCAP != CAP) {
         if (ok) k = (uint32_t)((u64)st[i] >> mb);
       } else {

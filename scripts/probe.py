@@ -39,7 +39,9 @@ for spec in sys.argv[1:]:
     c = CONFIGS[cfg]
     m = model_for(cfg)
     t0 = time.perf_counter()
-    ck = T.Checker(m, rank=rank, world=world,
+    eng = os.environ.get("PROBE_ENGINE", "auto")  # (global: the HBM-FPSet engine, pre-sized)
+    log2 = max(16, (2 * (c["distinct"] // world + 1) - 1).bit_length()) if eng == "global" else 0
+    ck = T.Checker(m, rank=rank, world=world, engine=eng, log2_fpset_slots=log2,
                    state_capacity=int(c["distinct"] * 1.15 / world) + (1 << 20))
     best, walls = 1e9, []
     for _ in range(reps):

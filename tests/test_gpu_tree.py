@@ -215,3 +215,35 @@ def test_tree_sharded_error_hands_over_to_the_exchange(case):
     assert r.engine == "global"
     assert r.status == want["result"] and r.depth == want["depth"]
     assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+
+
+def test_tree_closed_store_reads_back_states():
+    """the closed mode stores component codes (tree_body.h TLCG_TREE_CODE_STORE);
+    tlcg_copy_states / tlcg_state_at decode them: the first component's chunk
+    holds exactly its reachable states, each one's parent reference names a
+    state of the chunk that has it as a successor"""
+    c = GOLDEN["W_C12_k1"]["constants"]
+    m = model_of(c)
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run()
+        assert r.engine == "tree"
+        s0 = tlcgpu.host_init_state(m, 0)
+        seen, todo = set(), [s0]
+        while todo:
+            s = todo.pop()
+            if s not in seen:
+                seen.add(s)
+                todo += [t for _, t in tlcgpu.host_successors(m, s)]
+        n = len(seen)
+        assert n == r.distinct // tlcgpu.init_count(m)
+        stored = ck.copy_states(0, n)
+        assert set(stored) == seen and stored[0] == s0
+        ob = tlcgpu.load_library().tlcg_ordinal_bits(C.byref(m.to_c()))
+        for g in range(1, n, 7):
+            s, p = ck.state_at(g)
+            assert s == stored[g]
+            ps, _ = ck.state_at((p & ((1 << 56) - 1)) >> ob)
+            assert s in [t for _, t in tlcgpu.host_successors(m, ps)]
+    finally:
+        ck.close()
