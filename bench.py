@@ -438,12 +438,13 @@ def main():
 
     def roofline_tree(r):
         # SURVEY 8(d)'s per-unit figure x the distinct states of one step; the
-        # kernel writes the state word(s) and the parent entry per state (and,
-        # Producer modelled, a depth byte the next layer reads with the parent
-        # state, 9 B per entry); its FPSets stay in LDS
+        # kernel writes the parent entry per state and the state word (Producer
+        # modelled, plus a depth byte the next layer reads with the parent
+        # state, 9 B per entry) or, closed, the 4-B component code the host
+        # decodes (tree_body.h TLCG_TREE_CODE_STORE); its FPSets stay in LDS
         bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
-        per_state = BYTES_PER_STATE_WORD * (words + 1) + (1 if open_model else 0)
+        per_state = BYTES_PER_STATE_WORD * (words + 1) + 1 if open_model else 4 + BYTES_PER_STATE_WORD
         if open_model:
             kern = ("tlcg_tree_384 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<384, 512, 4> (") + \
                 "component tree, 4 components per wavefront)"

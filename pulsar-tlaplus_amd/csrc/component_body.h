@@ -78,6 +78,18 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 #ifndef TLCG_CODE_MAXLV
 #define TLCG_CODE_MAXLV 32
 #endif
+// component codes: the store slot of a state holds one 32-bit record
+// (comp_record, component.h: the code, the parent's queue position, the
+// action) instead of its state word and parent reference (16 B); the host
+// rebuilds both from the slot's component (comp_slot_decode).  G9: the two
+// 8-B stores cost 1.0 of 5.5 ms (TLCG_NO_STORE, profiles/r03j_probe.jsonl).
+// 0: words, for A/B (the host reads TLCG_JIT_DEFINES the same way)
+#ifndef TLCG_COMP_CODE_STORE
+#define TLCG_COMP_CODE_STORE 1
+#endif
+#ifndef TLCG_LVL_UNIFORM
+#define TLCG_LVL_UNIFORM 0
+#endif
 template <int K>
 struct CodeShape { static constexpr int T = (K * TLCG_CODE_FPSET_NUM / TLCG_CODE_FPSET_DEN + 15) / 16 * 16; };
 
@@ -163,6 +175,8 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     char* const stb = reinterpret_cast<char*>(a.store + b * (u64)K * 64);
     char* const parb = reinterpret_cast<char*>(a.parents + b * (u64)K * 64);
     const u64 pref = a.rank_tag | (gbase << L.ord_bits);
+    constexpr bool CREC = CODE && TLCG_COMP_CODE_STORE;  // 32-bit records (comp_record)
+    char* const recb = reinterpret_cast<char*>(reinterpret_cast<uint32_t*>(a.store) + b * (u64)K * 64);
     int head = 0, tail = 0, level = 0, lvl_end = 0, lvl_start = 0;
     // alive: the BFS goes on; stop: an error was found, so (like the level
     // loop of the global engine) the lane finishes expanding the current level
@@ -189,8 +203,12 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
 #endif
       Q(0) = k0;
       tail = 1;
-      st[0] = s0;
-      par[0] = NO_PARENT;
+      if constexpr (CREC) {
+        reinterpret_cast<uint32_t*>(recb)[lane] = comp_record(k0, 0, 0);  // (position 0: the root)
+      } else {
+        st[0] = s0;
+        par[0] = NO_PARENT;
+      }
       lgen = 1;
       int c;
       if constexpr (CODE) c = check_invariants_c(L, ccon, k0);
@@ -207,11 +225,15 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     auto insert = [&](lkey key, int action, int pos) -> int {
       Q(tail) = (qword)key;
 #ifndef TLCG_NO_STORE  // (experiment only: measures what the HBM store costs)
-      const unsigned off = (unsigned)(tail * 64 + lane) * 8u;
-      lkey lk = key;
-      if constexpr (CODE) lk = code_decode(L, ccon, key);
-      *reinterpret_cast<u64*>(stb + off) = msgs | ((u64)lk << mb);
-      *reinterpret_cast<u64*>(parb + off) = (pref + ((u64)pos << (6 + L.ord_bits))) | (u64)ordinal_of(L, action, 0);
+      if constexpr (CREC) {
+        *reinterpret_cast<uint32_t*>(recb + (unsigned)(tail * 64 + lane) * 4u) = comp_record(key, pos, action);
+      } else {
+        const unsigned off = (unsigned)(tail * 64 + lane) * 8u;
+        lkey lk = key;
+        if constexpr (CODE) lk = code_decode(L, ccon, key);
+        *reinterpret_cast<u64*>(stb + off) = msgs | ((u64)lk << mb);
+        *reinterpret_cast<u64*>(parb + off) = (pref + ((u64)pos << (6 + L.ord_bits))) | (u64)ordinal_of(L, action, 0);
+      }
 #endif
       ++tail;
 #ifdef TLCG_NO_INV  // (experiment only: measures what the invariants cost)
@@ -409,8 +431,34 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       bool brk = head >= tail;  // the component ran out
       if (head == lvl_end) {  // level `level` = [lvl_start, lvl_end) is complete, and expanded
 #ifndef TLCG_NO_LVL
-        atomicAdd(&lvl_sh[level < LV ? level : LV - 1],
-                  level >= counted ? (unsigned long long)(lvl_end - lvl_start) | ((unsigned long long)lvgen << 32) : 0ull);
+        {
+          const int lvc = level < LV ? level : LV - 1;
+          const unsigned long long lv =
+              level >= counted ? (unsigned long long)(lvl_end - lvl_start) | ((unsigned long long)lvgen << 32) : 0ull;
+#if TLCG_LVL_UNIFORM
+          // the lanes of a wave run isomorphic components in lockstep, so all
+          // 64 mostly close the same level at once: then one lane adds the
+          // wave's sum (a DPP scan per row of 16, the four row sums read
+          // into scalars) instead of 64 adds to one LDS address, which the
+          // LDS serializes (SQ_LDS_BANK_CONFLICT).  The halves are packed in
+          // 16 bits: <= 64 states and <= 256 successors per lane and level (K <= 64)
+          const int lv0 = __builtin_amdgcn_readfirstlane(lvc);
+          if (K <= 64 && __ballot(lvc == lv0) == ~0ull) {
+            unsigned x = level >= counted ? (unsigned)(lvl_end - lvl_start) | (lvgen << 16) : 0u;
+            x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+            x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+            x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+            x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
+            const unsigned s = (unsigned)__builtin_amdgcn_readlane((int)x, 15) + (unsigned)__builtin_amdgcn_readlane((int)x, 31) +
+                               (unsigned)__builtin_amdgcn_readlane((int)x, 47) + (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+            if (lane == 0) atomicAdd(&lvl_sh[lv0], (unsigned long long)(s & 0xFFFFu) | ((unsigned long long)(s >> 16) << 32));
+          } else {
+            atomicAdd(&lvl_sh[lvc], lv);
+          }
+#else
+          atomicAdd(&lvl_sh[lvc], lv);
+#endif
+        }
 #endif
         lgen += lvgen;
         lvgen = 0;

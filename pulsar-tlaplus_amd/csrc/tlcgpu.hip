@@ -854,6 +854,7 @@ struct tlcg_ctx {
     int K;
     u64 store_base, r0, n;
     std::vector<u64> list;  // initial-state indices (cascade passes); empty: range [r0, r0 + n)
+    bool codes = false;     // the store holds 32-bit records (comp_record), not words + parents
   };
   std::vector<CompPass> passes;
   std::vector<u64> comp_levels;
@@ -1630,7 +1631,43 @@ u128 tree_code_word(const tlcg_ctx* c, u64 g, uint32_t code) {
   return code_word<u128>(L, kc, s0 & messages_mask<u128>(L), code);
 }
 
+// the component-engine pass whose store holds 32-bit records (comp_record)
+// at slot g, or null
+const tlcg_ctx::CompPass* comp_code_pass(const tlcg_ctx* c, u64 g) {
+  if (c->engine != TLCG_ENGINE_COMPONENT) return nullptr;
+  for (const auto& ps : c->passes)
+    if (ps.codes && g >= ps.store_base && g < ps.store_base + component_store_slots(ps.n, ps.K)) return &ps;
+  return nullptr;
+}
+
+// the state word and parent reference of slot g of such a pass, from its
+// record: the slot names the batch, queue position and lane, so the lane's
+// component (its `messages` and code constants) and the parent's slot
+u64 comp_slot_decode(const tlcg_ctx* c, const tlcg_ctx::CompPass& ps, u64 g, uint32_t rec, u64* p) {
+  const Layout& L = c->hm.L;
+  const u64 off = g - ps.store_base, row = (u64)ps.K * 64;
+  const u64 b = off / row, lane = off % 64;
+  const u64 pos = off % row / 64, ci = b * 64 + lane;
+  const u64 idx0 = ps.list.empty() ? ps.r0 + ci : ps.list[ci] & ((1ull << 40) - 1);
+  const u64 s0 = init_state(L, idx0);
+  const CodeConsts kc = code_consts(L, comp_msgs_init(L, s0));
+  const int mb = L.msg_sh + L.N * L.mw;
+  if (p) {
+    const u64 gp = ps.store_base + b * row + ((rec >> 16) & 255) * 64 + lane;
+    *p = pos == 0 ? NO_PARENT
+                  : ((u64)c->opts.rank << 56) | (gp << L.ord_bits) | (u64)ordinal_of(L, (int)(rec >> 24), 0);
+  }
+  return (s0 & L.msgs_mask) | ((u64)code_decode(L, kc, (ckey)(rec & 0xFFFF)) << mb);
+}
+
 bool state_at(tlcg_ctx* c, u64 g, u128* s, u64* p) {
+  if (const tlcg_ctx::CompPass* ps = comp_code_pass(c, g)) {
+    uint32_t rec = 0;
+    HIPCHK(hipMemcpy(&rec, reinterpret_cast<const uint32_t*>(c->d_states + ps->store_base) + (g - ps->store_base), 4,
+                     hipMemcpyDeviceToHost));
+    *s = comp_slot_decode(c, *ps, g, rec, p);
+    return true;
+  }
   if (c->tree_codes) {
     uint32_t code = 0;
     HIPCHK(hipMemcpy(&code, reinterpret_cast<const uint32_t*>(c->d_states) + g, 4, hipMemcpyDeviceToHost));
@@ -1858,7 +1895,13 @@ int run_component(tlcg_ctx* c) {
     const u64 base = c->comp_store_used;
     const u64 slots = component_store_slots(n, K);
     if (!ensure_store(c, base + slots)) return -1;
+    // the first pass runs component codes when they fit 16 bits (component_code.h);
+    // a component whose initial key is no code, and the cascade, run 32-bit keys
+    const bool code = p == 0 && K <= 64 && c->comp_code;
     tlcg_ctx::CompPass pass{K, base, r0, n, {}};
+    // (its store holds records unless an A/B build of the specialized kernels asked for words)
+    const char* jd = std::getenv("TLCG_JIT_DEFINES");
+    pass.codes = code && !(c->jit_used && jd && std::strstr(jd, "TLCG_COMP_CODE_STORE=0"));
     if (cur >= 0) {
       pass.list.resize(n);
       HIPCHK_I(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
@@ -1886,9 +1929,6 @@ int run_component(tlcg_ctx* c) {
     a.stripe = kCompCounters;
     a.nstripe = COMP_STRIPES;
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
-    // the first pass runs component codes when they fit 16 bits (component_code.h);
-    // a component whose initial key is no code, and the cascade, run 32-bit keys
-    const bool code = p == 0 && K <= 64 && c->comp_code;
     // the code pass's slot hash, tuned on one component (all share its code graph)
     a.mult = code ? c->comp_mult : DEFAULT_SLOT_MULT;
     if (!(c->jit_used ? jit_launch_component(c->jit, a, K, code, c->stream) : launch_component(a, K, code, c->stream))) {
@@ -2732,6 +2772,32 @@ int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* ou
   const DeviceGuard dg(c);
   if (!c || first + n > store_end(c)) return -1;
   const u64 w = c->words;
+  if (c->engine == TLCG_ENGINE_COMPONENT) {  // record slots decoded here, word slots copied
+    while (n) {
+      u64 m = n;
+      if (const tlcg_ctx::CompPass* ps = comp_code_pass(c, first)) {
+        m = std::min<u64>(n, ps->store_base + component_store_slots(ps->n, ps->K) - first);
+        std::vector<uint32_t> rec(m);
+        if (hipMemcpy(rec.data(), reinterpret_cast<const uint32_t*>(c->d_states + ps->store_base) + (first - ps->store_base),
+                      m * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+          c->err = "copy failed";
+          return -10;
+        }
+        for (u64 i = 0; i < m; ++i) out[i] = comp_slot_decode(c, *ps, first + i, rec[i], nullptr);
+      } else {
+        for (const auto& ps : c->passes)  // up to the next record pass
+          if (ps.codes && ps.store_base > first) m = std::min<u64>(m, ps.store_base - first);
+        if (hipMemcpy(out, dev_state(c, first), m * 8 * w, hipMemcpyDeviceToHost) != hipSuccess) {
+          c->err = "copy failed";
+          return -10;
+        }
+      }
+      out += m * w;
+      first += m;
+      n -= m;
+    }
+    return 0;
+  }
   if (c->tree_codes) {  // component codes: decoded here
     std::vector<uint32_t> codes(n);
     if (n && hipMemcpy(codes.data(), reinterpret_cast<const uint32_t*>(c->d_states) + first, n * 4,

@@ -260,6 +260,58 @@ def test_g9_component_engine():
         ck.close()
 
 
+@pytest.mark.parametrize("jit", ["0", "1"])
+def test_component_code_records_decode(jit, monkeypatch):
+    """The code pass stores one 32-bit record per state (csrc/component.h
+    comp_record: code, parent queue position, action) and tlcg_state_at /
+    tlcg_copy_states rebuild the state word and the parent reference from the
+    slot: component ci (lane ci % 64 of batch ci // 64) reads back, at
+    positions 0..n-1, exactly its n reachable states in BFS order, position 0
+    its initial state without a parent, every other state a successor of an
+    earlier position of the same lane by the recorded action.  Precompiled
+    (TLCG_JIT=0) and hipRTC-specialized (1) kernels."""
+    monkeypatch.setenv("TLCG_JIT", jit)
+    m = model_of(GOLDEN["X_keys3_vals57"]["constants"])
+    ck = tlcgpu.Checker(m, engine="component")
+    try:
+        r = ck.run(with_trace=False)
+        assert r.engine == "component"
+        check_against_golden("X_keys3_vals57", r, False)
+        lib = tlcgpu.load_library()
+        import ctypes
+        ob = lib.tlcg_ordinal_bits(ctypes.byref(m.to_c()))
+        n_init = tlcgpu.init_count(m)
+        checked = 0
+        for ci in list(range(0, min(n_init, 130))) + [n_init - 1]:
+            seen, order = {tlcgpu.host_init_state(m, ci)}, [tlcgpu.host_init_state(m, ci)]
+            for s in order:  # the component's closure (no Producer: `messages` is fixed)
+                for _, t in tlcgpu.host_successors(m, s):
+                    if t not in seen:
+                        seen.add(t)
+                        order.append(t)
+            if len(order) > 62:  # (K - 1 or more states: the cascade's word store)
+                continue
+            base = (ci // 64) * 64 * 64 + ci % 64
+            slots = [base + 64 * p for p in range(len(order))]
+            got = ck.copy_states(slots[0], slots[-1] - slots[0] + 1)[::64]
+            assert set(got) == seen and got[0] == order[0]
+            for p, g in enumerate(slots):
+                s, pref = ck.state_at(g)
+                assert s == got[p]
+                if p == 0:
+                    assert pref == (1 << 64) - 1
+                    continue
+                pg, ordinal = (pref & ((1 << 56) - 1)) >> ob, pref & ((1 << ob) - 1)
+                assert pg in slots[:p]
+                ps, _ = ck.state_at(pg)
+                act = tlcgpu.ACTIONS[lib.tlcg_action_of_ordinal(ctypes.byref(m.to_c()), ordinal)]
+                assert (act, s) in tlcgpu.host_successors(m, ps)
+            checked += 1
+        assert checked > 100
+    finally:
+        ck.close()
+
+
 def test_component_engine_multi_rank_ranges():
     m = model_of(GOLDEN["X_keys3_vals57"]["constants"])
     want = GOLDEN["X_keys3_vals57"]["result"]
