@@ -7,9 +7,12 @@ MaxCrashTimes = 1, RetainNullKey, no producer/consumer -> 1,040,187,392
 distinct states, 1,392,508,928 generated, depth 20): FPSet cleared, Init,
 then every BFS level until the queue is empty.  Inputs are the constants;
 everything lives in HBM.  With N GPUs the same job is split across N ranks
-(strong scaling), the FPSet hash-partitioned by owner (dist.py).
+(strong scaling): without a Producer each rank runs a contiguous range of the
+components (no data-path collective); the FPSet hash-partitioned by owner
+with the per-level exchange (BASELINE config 4) is measured beside it, and a
+producer-modelled cfg splits the component tree by subtrees.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config g9|m8|s]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config g9|m8|s|g9deep|p8]
 """
 import argparse
 import json
@@ -41,7 +44,7 @@ BYTES_PER_STATE_WORD = 8
 # the newest round's profile of each kind (profiles/rNN_*), measured on the same kernels
 PMC_PROFILE = "pmc_k_expand.json"
 PMC_COMPONENT_PROFILE = "pmc_component.json"
-COMPONENT_BYTES_PER_STATE = 16  # state word + parent entry written to the HBM store
+COMPONENT_BYTES_PER_STATE = 4  # the code pass writes one 32-bit record per state (component.h comp_record)
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
 # algorithmic HBM bytes per distinct state of the BFS path (read
 # the frontier state 8 B, write the new state 8 B and its parent entry 8 B,
@@ -395,7 +398,8 @@ def main():
 
     def roofline_component(r):
         # SURVEY 8(d)'s per-unit figure x the distinct states of one launch; the
-        # kernel itself only writes 16 B/state (the FPSet and queue stay on chip)
+        # kernel itself only writes a 4-B record per state (the FPSet and queue
+        # stay on chip; the 32-bit cascade passes, none on G9, write 16 B)
         bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
         achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
         written = COMPONENT_BYTES_PER_STATE * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
