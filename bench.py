@@ -328,32 +328,13 @@ def main():
                              "(16-B records) + ncclAllReduce per level, RCCL over xGMI")
 
     open_model = bool(cfg.get("producer"))
-    exchange_run = global_run = None
-    exchange_error = None
+    global_run = None
     if open_model and distributed:
         # the component tree split by subtrees (no exchange), or the level loop's exchange if it hands over
         main_run = time_exchange(0)
     else:
         main_run = time_engine("auto")
         global_run = time_engine("global")  # the HBM-FPSet engine beside the on-chip one
-        if distributed and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
-            # a secondary measurement: its failure (every rank learns of it
-            # through torch's own group) must not cost the headline line
-            try:
-                exchange_run = time_exchange(2)
-                ok = 1
-            except (Exception, SystemExit) as e:  # noqa: BLE001
-                exchange_error = f"{type(e).__name__}: {e}"[:300]
-                ok = 0
-            flag = torch.tensor([ok], dtype=torch.int64, device=rdev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if not int(flag.item()):
-                exchange_run = None
-                exchange_error = exchange_error or "failed on another rank"
-    if rank != 0:
-        if distributed:
-            dist.destroy_process_group()
-        return
     distinct, generated = cfg["distinct"], cfg["generated"]
     # (a producer-modelled cfg has one initial state; its Terminating stutters
     # are not counted out of the probes, so its bytes/state is an upper bound)
@@ -477,39 +458,75 @@ def main():
         return out
 
     main_s = summary(main_run)
-    line = {
-        "metric": "distinct states/sec, compaction.tla scaled cfg, 1/2/4/8 MI355X vs host TLC",
-        "value": main_s["value"],
-        "unit": "distinct states/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": main_s["ms_per_step"],
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic: the model's own state space (no external data)",
-        "config": {"workload": f"compaction.tla BFS, {args.config.upper()} cfg: KeySpace = ValueSpace = "
-                               f"{{1..{cfg['keys']}}}, MessageSentLimit 3, CompactionTimesLimit {cfg.get('C', 3)}, "
-                               f"MaxCrashTimes 1, RetainNullKey {'FALSE' if cfg.get('retain') is False else 'TRUE'}, "
-                               f"{'ModelProducer' if open_model else 'no producer'}, no consumer",
-                   "state_bits": tlcgpu.state_bits(model),
-                   "distinct": distinct, "generated": generated, "depth": cfg["depth"],
-                   "parallelism": f"partition{world}", "engine": main_s["engine"],
-                   "gpu_kernel_ms_per_step": main_s["gpu_kernel_ms_per_step"]},
-        "roofline": main_s["roofline"],
-        "engines": {},
-    }
-    if global_run:
-        line["engines"]["global_hbm_fpset"] = summary(global_run)
-    if exchange_run:
-        line["engines"]["global_open_partition_alltoall"] = summary(exchange_run)
-    elif exchange_error:
-        line["engines"]["global_open_partition_alltoall"] = {"error": exchange_error}
-    if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.config)
-    print(json.dumps(line), flush=True)
+
+    def build_line(exchange_run, exchange_error):
+        line = {
+            "metric": "distinct states/sec, compaction.tla scaled cfg, 1/2/4/8 MI355X vs host TLC",
+            "value": main_s["value"],
+            "unit": "distinct states/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": main_s["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: the model's own state space (no external data)",
+            "config": {"workload": f"compaction.tla BFS, {args.config.upper()} cfg: KeySpace = ValueSpace = "
+                                   f"{{1..{cfg['keys']}}}, MessageSentLimit 3, CompactionTimesLimit {cfg.get('C', 3)}, "
+                                   f"MaxCrashTimes 1, RetainNullKey {'FALSE' if cfg.get('retain') is False else 'TRUE'}, "
+                                   f"{'ModelProducer' if open_model else 'no producer'}, no consumer",
+                       "state_bits": tlcgpu.state_bits(model),
+                       "distinct": distinct, "generated": generated, "depth": cfg["depth"],
+                       "parallelism": f"partition{world}", "engine": main_s["engine"],
+                       "gpu_kernel_ms_per_step": main_s["gpu_kernel_ms_per_step"]},
+            "roofline": main_s["roofline"],
+            "engines": {},
+        }
+        if global_run:
+            line["engines"]["global_hbm_fpset"] = summary(global_run)
+        if exchange_run:
+            line["engines"]["global_open_partition_alltoall"] = summary(exchange_run)
+        elif exchange_error:
+            line["engines"]["global_open_partition_alltoall"] = {"error": exchange_error}
+        return line
+
+    exchange_run = exchange_error = None
+    if distributed and not open_model and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
+        # a secondary measurement (BASELINE config 4): its failure (every rank
+        # learns of it through torch's own group) must not cost the headline
+        # line, and neither may a hang -- the library aborts a collective after
+        # TLCG_COMM_TIMEOUT_S, and this watchdog ends the job with the headline
+        # line if the whole leg outlives TLCG_BENCH_EXCHANGE_TIMEOUT_S
+        limit = float(os.environ.get("TLCG_BENCH_EXCHANGE_TIMEOUT_S", "240"))
+
+        def bail():
+            if rank == 0:
+                print(json.dumps(build_line(None, f"the exchange leg did not finish within {limit:.0f} s")), flush=True)
+            os._exit(0)
+
+        import threading
+        watchdog = threading.Timer(limit, bail)
+        watchdog.daemon = True
+        watchdog.start()
+        try:
+            exchange_run = time_exchange(2)
+            ok = 1
+        except (Exception, SystemExit) as e:  # noqa: BLE001
+            exchange_error = f"{type(e).__name__}: {e}"[:300]
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int64, device=rdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        watchdog.cancel()
+        if not int(flag.item()):
+            exchange_run = None
+            exchange_error = exchange_error or "failed on another rank"
+    if rank == 0:
+        line = build_line(exchange_run, exchange_error)
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.config)
+        print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
 

@@ -356,9 +356,20 @@ int tlcg_partition_closed(const tlcg_ctx* c);
  * forces one; st->transport says which ran).  *st gets the combined verdict
  * (the first error by level then rank, every rank's counts cut at the end of
  * its level; level sizes summed into levels[0..cap), *n_levels).  The
- * contexts are destroyed before return; a trace is re-derived on one GPU. */
+ * contexts are destroyed before return (tlcg_run_node_trace also returns the
+ * counterexample; TLC's own -workers 1 trace is re-derived on one GPU). */
 int tlcg_run_node(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_stats* st, uint64_t* levels,
                   int32_t cap, int32_t* n_levels, char* err, int32_t err_cap);
+/* tlcg_run_node plus the first error's counterexample without a re-run
+ * (SURVEY 8(e)): the parent references walked across the ranks' stores,
+ * host-mediated (each hop's owner reads the state, the transport hands it to
+ * every rank).  states[i * words ..] (tlcg_state_words) and actions[i]
+ * (TLCG_ACT_*, TLCG_ACT_INIT for the first) for i < min(*trace_len,
+ * trace_cap); *trace_len = 0 when the model holds.  A shortest
+ * counterexample; TLC -workers 1's own one needs TLC order on one GPU. */
+int tlcg_run_node_trace(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_stats* st, uint64_t* levels,
+                        int32_t cap, int32_t* n_levels, uint64_t* states, int32_t* actions, int32_t trace_cap,
+                        int32_t* trace_len, char* err, int32_t err_cap);
 
 /* ---- one process per GPU over RCCL (xGMI) ----
  * Rank 0 calls tlcg_comm_unique_id and hands the 128 bytes to every rank (the
@@ -370,7 +381,9 @@ int tlcg_run_node(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_stats
  * ncclSend/ncclRecv of the 16-B records -> absorb, with an ncclAllReduce
  * deciding termination.  *st and levels[0..*n_levels) are the combined result
  * (the same on every rank; the first error by level, then rank, with every
- * rank's counts cut at the end of its level).  A collective that does not
+ * rank's counts cut at the end of its level); on an error every rank's
+ * tlcg_trace_words then returns the counterexample walked across the ranks'
+ * stores (tlcg_run_node_trace).  A collective that does not
  * complete within TLCG_COMM_TIMEOUT_S seconds (default 600) aborts the
  * communicator and returns an error.  RCCL is loaded at run time
  * (librccl.so.1); tlcg_comm_available says whether it can be. */

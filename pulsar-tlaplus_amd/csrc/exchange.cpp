@@ -567,7 +567,10 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
   out.distinct = 0;
   for (uint64_t x : lv) out.distinct += x;
   out.frontier = first < 0 || lv.empty() ? 0 : lv.back();
-  out.depth = first < 0 ? (int32_t)lv.size() : (int32_t)cut;
+  // (an open partition's ranks keep empty levels, tlcg_end_level: the
+  // erroring rank's level count may hold an empty last level, which one
+  // context would not have pushed -- the summed sizes decide)
+  out.depth = (int32_t)lv.size();
   out.status = first < 0 ? TLCG_DONE : (int32_t)info[1];
   out.invariant = (int32_t)info[2] - 1;
   out.action = (int32_t)info[3] - 1;
@@ -580,6 +583,9 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
   const double d = (double)out.distinct, gg = (double)out.generated;
   out.fp_collision_optimistic = d * (gg - d) / 18446744073709551616.0;
   out.transport = comm_transport(c) == &t ? 2 : 1;
+  // the counterexample, walked across the ranks' stores: every rank can then
+  // return it (tlcg_trace_words) without a re-run on one GPU
+  if (first >= 0 && !trace_ranks(c, t, first, err)) return -20;
   *st = out;
   if (levels) *levels = lv;
   return 0;

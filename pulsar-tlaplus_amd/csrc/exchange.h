@@ -57,6 +57,10 @@ int comm_init_all(tlcg_ctx* const* ctxs, int n, std::string* err);
 Transport* comm_transport(tlcg_ctx* c);  // the context's RCCL transport, or null
 void comm_free(void* comm_state);
 
+// the first error's counterexample walked across the ranks' stores (tlcgpu.hip;
+// collective over t, after run_ranks has combined the result)
+bool trace_ranks(tlcg_ctx* c, Transport& t, int first, std::string* err);
+
 // context internals exchange.cpp needs (tlcgpu.hip)
 int ctx_device(const tlcg_ctx* c);
 int ctx_engine(const tlcg_ctx* c);         // TLCG_ENGINE_* of the last tlcg_init

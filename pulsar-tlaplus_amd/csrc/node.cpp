@@ -38,6 +38,14 @@ void put_err(char* err, int32_t cap, const std::string& s) {
 
 extern "C" int tlcg_run_node(const tlcg_model* m, const tlcg_opts* base, int32_t n, tlcg_stats* st,
                              uint64_t* levels_out, int32_t cap, int32_t* n_levels, char* err, int32_t err_cap) {
+  return tlcg_run_node_trace(m, base, n, st, levels_out, cap, n_levels, nullptr, nullptr, 0, nullptr, err, err_cap);
+}
+
+extern "C" int tlcg_run_node_trace(const tlcg_model* m, const tlcg_opts* base, int32_t n, tlcg_stats* st,
+                                   uint64_t* levels_out, int32_t cap, int32_t* n_levels, uint64_t* states,
+                                   int32_t* actions, int32_t trace_cap, int32_t* trace_len, char* err,
+                                   int32_t err_cap) {
+  if (trace_len) *trace_len = 0;
   if (!m || !base || !st || n < 1 || n > 64) {
     put_err(err, err_cap, "tlcg_run_node: bad arguments");
     return -1;
@@ -96,6 +104,12 @@ extern "C" int tlcg_run_node(const tlcg_model* m, const tlcg_opts* base, int32_t
   if (levels_out)
     for (size_t i = 0; i < lv.size() && (int32_t)i < cap; ++i) levels_out[i] = lv[i];
   if (n_levels) *n_levels = (int32_t)lv.size();
+  // the first error's counterexample, walked across the ranks' stores by
+  // run_ranks (every rank holds it)
+  if (trace_len && st->status >= TLCG_VIOLATION) {
+    int32_t tn = 0;
+    if (tlcg_trace_words(ctxs[0], states, actions, trace_cap, &tn) == 0) *trace_len = tn;
+  }
   destroy_all();
   return 0;
 }

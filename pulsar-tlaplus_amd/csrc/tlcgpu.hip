@@ -905,6 +905,11 @@ struct tlcg_ctx {
   u64 ev_parent_gidx = NO_PARENT;
   u64 ev_parent_ref = NO_PARENT;
   int ev_action = -1;
+  // the counterexample of a multi-rank run, walked across the ranks' stores
+  // by trace_ranks (every rank holds it); tlcg_trace_words returns it
+  bool xtrace_valid = false;
+  std::vector<u128> xtrace_states;
+  std::vector<int> xtrace_acts;
   double kernel_ms = 0, expand_ms = 0;
   u64 levels_redone = 0;
   u64 owner_mask = ~0ull;
@@ -2505,6 +2510,93 @@ bool step_level(tlcg_ctx* c) {
 
 }  // namespace
 
+namespace tlcg {
+
+// The counterexample of a multi-rank run (the parent references
+// walked across the ranks' stores, host-mediated).  Collective: every rank of
+// t calls it with the same `first` (the rank holding the first error,
+// run_ranks); each hop's owner reads the state and its parent reference from
+// its store and an all-reduce (sum; the other ranks add zeros) hands them to
+// every rank.  A parent reference names its rank (bits 56..63), so the walk
+// follows states absorbed from other ranks back to their discoverers.  On
+// success every rank holds the trace (tlcg_trace_words); false only on a
+// transport failure (a state the owner cannot read ends the walk: no trace).
+bool trace_ranks(tlcg_ctx* c, Transport& t, int first, std::string* err) {
+  const Layout& L = c->hm.L;
+  const int me = t.rank(), w = c->words;
+  const u64 ordmask = (1ull << L.ord_bits) - 1, refmask = (1ull << 56) - 1;
+  c->xtrace_valid = false;
+  c->xtrace_states.clear();
+  c->xtrace_acts.clear();
+  // the event: level, status, action, its parent reference, the event state
+  uint64_t ev[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (me == first) {
+    u64 sw[2] = {0, 0};
+    split_words(c->ev_state, sw, w);
+    ev[0] = (u64)(c->ev_level + 1);
+    ev[1] = (u64)c->status;
+    ev[2] = (u64)(c->ev_action + 2);  // (TLCG_ACT_INIT = -1)
+    ev[3] = c->ev_parent_gidx != NO_PARENT ? ((u64)c->opts.rank << 56) | (c->ev_parent_gidx << L.ord_bits)
+                                           : c->ev_parent_ref;
+    ev[4] = sw[0];
+    ev[5] = sw[1];
+    ev[6] = 1;
+  }
+  if (!t.allreduce(ev, 7, RED_SUM, err)) return false;
+  if (ev[6] != 1 || ev[0] == 0) return true;  // (no event on `first`: no trace)
+  u64 evw[2] = {ev[4], ev[5]};
+  const u128 ev_state = join_words(evw, w);
+  const int level = (int)ev[0] - 1, status = (int)ev[1], action = (int)ev[2] - 2;
+  std::vector<u128> st;
+  std::vector<int> act;
+  if (level == 0) {
+    st.push_back(ev_state);
+    act.push_back(TLCG_ACT_INIT);
+  } else {
+    u64 ref = ev[3];
+    for (int hop = 0;; ++hop) {
+      if (ref == NO_PARENT || hop > (1 << 16)) return true;  // (a broken chain: no trace)
+      const int owner = (int)(ref >> 56);
+      const u64 g = (ref & refmask) >> L.ord_bits;
+      uint64_t msg[4] = {0, 0, 0, 0};  // ok, parent reference, state words
+      if (me == owner) {
+        u128 s = 0;
+        u64 p = 0;
+        if (g < store_end(c) && state_at(c, g, &s, &p)) {
+          u64 sw[2] = {0, 0};
+          split_words(s, sw, w);
+          msg[0] = 1;
+          msg[1] = p;
+          msg[2] = sw[0];
+          msg[3] = sw[1];
+        }
+      }
+      if (!t.allreduce(msg, 4, RED_SUM, err)) return false;
+      if (msg[0] != 1) return true;
+      u64 sw[2] = {msg[2], msg[3]};
+      st.push_back(join_words(sw, w));
+      if (msg[1] == NO_PARENT) {
+        act.push_back(TLCG_ACT_INIT);
+        break;
+      }
+      act.push_back(action_of_ordinal(L, (int)(msg[1] & ordmask)));
+      ref = msg[1];
+    }
+    std::reverse(st.begin(), st.end());
+    std::reverse(act.begin(), act.end());
+    if (status == TLCG_VIOLATION || status == TLCG_INVARIANT_ERROR) {
+      st.push_back(ev_state);
+      act.push_back(action);
+    }
+  }
+  c->xtrace_states = std::move(st);
+  c->xtrace_acts = std::move(act);
+  c->xtrace_valid = true;
+  return true;
+}
+
+}  // namespace tlcg
+
 extern "C" {
 
 int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
@@ -2661,6 +2753,7 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
   free_tier(c);
   free_host_chunks(c);
   c->tree_codes = false;
+  c->xtrace_valid = false;
   c->kernel_ms = c->expand_ms = 0;
   c->status = TLCG_RUNNING;
   c->ev_word = NO_EVENT;
@@ -2834,6 +2927,15 @@ int tlcg_copy_states(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* out) {
 int tlcg_trace_words(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int32_t* len) {
   const DeviceGuard dg(c);
   if (!c) return -1;
+  if (c->xtrace_valid) {  // a multi-rank run's counterexample (trace_ranks)
+    const int n = (int)c->xtrace_states.size();
+    for (int i = 0; i < n && i < cap; ++i) {
+      if (states) split_words(c->xtrace_states[(size_t)i], states + (size_t)i * c->words, c->words);
+      if (actions) actions[i] = c->xtrace_acts[(size_t)i];
+    }
+    if (len) *len = n;
+    return 0;
+  }
   if (c->ev_word == NO_EVENT) {
     c->err = "no violation to trace";
     return -2;

@@ -250,9 +250,18 @@ int main(int argc, char** argv) {
   else std::printf("Computing initial states...\n");
   tlcg_ctx* ctx = nullptr;
   tlcg_stats st;
+  // -gpus N: the first error's counterexample walked across the ranks' stores
+  // (printed when the one-GPU TLC-order re-run below cannot be made)
+  const int state_words = tlcg_state_words(&model);
+  std::vector<uint64_t> node_states;
+  std::vector<int32_t> node_acts;
+  int32_t node_tlen = 0;
   if (o.gpus > 1) {
     char merr[512];
-    if (tlcg_run_node(&model, &opts, o.gpus, &st, nullptr, 0, nullptr, merr, sizeof merr) != 0) {
+    node_states.resize((size_t)state_words << 16);
+    node_acts.resize(1 << 16);
+    if (tlcg_run_node_trace(&model, &opts, o.gpus, &st, nullptr, 0, nullptr, node_states.data(), node_acts.data(),
+                            (int32_t)node_acts.size(), &node_tlen, merr, sizeof merr) != 0) {
       std::printf("Error: %s\n", merr);
       return 255;
     }
@@ -365,7 +374,7 @@ int main(int argc, char** argv) {
     // TLC prints the trace of the first error in its (one-worker) order: reproduce it
     tlcg_ctx* tctx = ctx;
     tlcg_stats tst = st;
-    bool own = false;
+    bool own = false, use_node_trace = false;
     // (after -gpus N: on one GPU).  The global engine in TLC order stores the
     // states in TLC's FIFO order, which also gives TLC's statistics at the stop.
     if (o.trace && (!o.tlc_order || !ctx || st.engine != TLCG_ENGINE_GLOBAL)) {
@@ -388,10 +397,18 @@ int main(int argc, char** argv) {
         tst = st;
         // fall back to the first run's engine and order: a shortest
         // counterexample, but not necessarily the one TLC -workers 1 prints
+        // (-gpus N: the one walked across the ranks' stores, no re-run)
+        if (o.gpus > 1 && node_tlen > 0) {
+          use_node_trace = true;
+          std::printf("Warning: the TLC-order re-run for the trace failed (%s); the trace below is a shortest "
+                      "counterexample (walked across the GPUs' stores) but may not be the one TLC prints, and the "
+                      "counts are at the end of the level.\n", why.c_str());
+        }
         tlcg_opts fo = opts;
         if (!o.recover.empty() || o.gpus > 1) fo.engine = TLCG_ENGINE_GLOBAL;
         tlcg_stats fst;
-        if (tlcg_create(&model, &fo, &tctx) == 0 && tlcg_run(tctx, &fst) == 0 && fst.status == st.status) {
+        if (use_node_trace) {
+        } else if (tlcg_create(&model, &fo, &tctx) == 0 && tlcg_run(tctx, &fst) == 0 && fst.status == st.status) {
           own = true;
           std::printf("Warning: the TLC-order re-run for the trace failed (%s); the trace below is a shortest "
                       "counterexample but may not be the one TLC prints, and the counts are at the end of the "
@@ -423,12 +440,17 @@ int main(int argc, char** argv) {
         rc = 75;
         break;
     }
-    if (o.trace && tctx) {
-      const int words = tlcg_state_words(&model);  // 1, or 2 for a > 63-bit layout
+    if (o.trace && (tctx || use_node_trace)) {
+      const int words = state_words;  // 1, or 2 for a > 63-bit layout
       std::vector<uint64_t> states((size_t)words << 16);
       std::vector<int32_t> acts(1 << 16);
       int32_t n = 0;
-      if (tlcg_trace_words(tctx, states.data(), acts.data(), (int32_t)acts.size(), &n) == 0) {
+      if (use_node_trace) {
+        states = node_states;
+        acts = node_acts;
+        n = std::min<int32_t>(node_tlen, (int32_t)acts.size());
+      }
+      if (use_node_trace || tlcg_trace_words(tctx, states.data(), acts.data(), (int32_t)acts.size(), &n) == 0) {
         std::printf("Error: The behavior up to this point is:\n");
         std::vector<char> buf(1 << 16);
         for (int i = 0; i < n; ++i) {

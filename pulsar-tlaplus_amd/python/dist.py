@@ -22,8 +22,8 @@ engine wraps libtlcgpu, the tests plug a CPU stand-in into the same driver.
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass
-from typing import List, Optional
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -46,6 +46,7 @@ class DistResult:
     invariant: Optional[int] = None         # index into the model's invariants (first error)
     first_error_rank: Optional[int] = None
     engine: str = ""                         # "tree": the ranks ran shares of the component tree
+    trace: List[Tuple[str, int]] = field(default_factory=list)  # run_native: walked across the ranks' stores
 
 
 class GpuEngine:
@@ -191,10 +192,13 @@ def run_native(engine: "GpuEngine") -> DistResult:
     n = C.c_int32()
     engine.ck._chk(lib.tlcg_run_comm(engine.ctx, C.byref(st), lv, 65536, C.byref(n)), "tlcg_run_comm")
     levels = [lv[i] for i in range(n.value)]
+    trace = []
+    if st.status >= 2:  # an error: the counterexample walked across the ranks' stores (every rank holds it)
+        trace = engine.ck.trace()
     return DistResult(status=tlcgpu.STATUS[st.status], generated=st.generated, distinct=st.distinct, depth=st.depth,
                       levels=levels, kernel_ms=st.kernel_ms, expand_ms=st.expand_ms, closed=engine.closed,
                       invariant=st.invariant if st.invariant >= 0 else None,
-                      engine=tlcgpu.ENGINE_NAMES.get(int(st.engine), "?"))
+                      engine=tlcgpu.ENGINE_NAMES.get(int(st.engine), "?"), trace=trace)
 
 
 def _transport_device(group, dev: torch.device) -> torch.device:

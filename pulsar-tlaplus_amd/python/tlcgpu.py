@@ -135,6 +135,8 @@ def load_library(path: str = LIB_PATH):
         "tlcg_exchange_local": (C.c_int, [C.POINTER(P), I32, C.POINTER(U64)]),
         "tlcg_partition_closed": (C.c_int, [P]),
         "tlcg_run_node": (C.c_int, [M, O, I32, S, C.POINTER(U64), I32, C.POINTER(I32), C.c_char_p, I32]),
+        "tlcg_run_node_trace": (C.c_int, [M, O, I32, S, C.POINTER(U64), I32, C.POINTER(I32), C.POINTER(U64),
+                                          C.POINTER(I32), I32, C.POINTER(I32), C.c_char_p, I32]),
         "tlcg_comm_available": (C.c_int, []),
         "tlcg_comm_unique_id": (C.c_int, [P, I32]),
         "tlcg_comm_init": (C.c_int, [P, P, I32]),
@@ -534,8 +536,9 @@ def run_node(model: Model, ranks: int, device: int = 0, log2_fpset_slots: int = 
              partition: int = 0, engine: str = "auto", spill: bool = False, device_store_cap: int = 0,
              fpset_spill: bool = False, log2_fpset_max: int = 0) -> Result:
     """The check by this one process on `ranks` contexts, rank r on device
-    r mod device_count (tlcg_run_node; `tlc-hip -gpus N`).  No trace: on an
-    error it is re-derived on one GPU (Checker(..., tlc_order=True))."""
+    r mod device_count (tlcg_run_node_trace; `tlc-hip -gpus N`).  On an error
+    .trace is the counterexample walked across the ranks' stores (a shortest
+    one; TLC -workers 1's own trace: Checker(..., tlc_order=True))."""
     lib = load_library()
     m = model.to_c()
     o = tlcg_opts()
@@ -547,7 +550,13 @@ def run_node(model: Model, ranks: int, device: int = 0, log2_fpset_slots: int = 
     lv = (C.c_uint64 * 65536)()
     n = C.c_int32()
     err = C.create_string_buffer(1024)
-    rc = lib.tlcg_run_node(C.byref(m), C.byref(o), ranks, C.byref(st), lv, 65536, C.byref(n), err, 1024)
+    w = state_words(model)
+    tcap = 4096
+    tst = (C.c_uint64 * (tcap * w))()
+    tact = (C.c_int32 * tcap)()
+    tlen = C.c_int32()
+    rc = lib.tlcg_run_node_trace(C.byref(m), C.byref(o), ranks, C.byref(st), lv, 65536, C.byref(n), tst, tact, tcap,
+                                 C.byref(tlen), err, 1024)
     if rc != 0:
         raise RuntimeError(f"tlcg_run_node: {err.value.decode()} ({rc})")
     status = STATUS[st.status]
@@ -561,4 +570,6 @@ def run_node(model: Model, ranks: int, device: int = 0, log2_fpset_slots: int = 
         r.invariant = model.invariants[st.invariant]
     if st.action >= 0:
         r.action = ACTIONS[st.action]
+    r.trace = [("Init" if tact[i] < 0 else ACTIONS[tact[i]], _from_words(tst, i, w))
+               for i in range(min(tlen.value, tcap))]
     return r

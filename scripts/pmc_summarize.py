@@ -5,8 +5,11 @@ kernel trace, the issue fraction and the HBM bytes.
     python scripts/pmc_summarize.py DIR KSUB CASE [OUT.json]
 
 HBM bytes (MI355X_MICROARCH.md, HBM): FETCH_SIZE and WRITE_SIZE are in KB;
-on gfx950 FETCH_SIZE tallies 128-B read requests at 64 B, so it is doubled
-("fetch_bytes_corrected"); WRITE_SIZE is taken as is."""
+on gfx950 FETCH_SIZE tallies 128-B read requests of wide streaming reads at
+64 B, so it is doubled ("fetch_bytes_corrected"); WRITE_SIZE is taken as is.
+PMC_FETCH_SCALE=1 keeps FETCH_SIZE as counted: scattered 8-B loads count one
+64-B request each (profiles/r03_pmc_calibration.json), so a probe-bound
+kernel (k_expand_fast) is summarized with it."""
 import collections
 import csv
 import glob
@@ -31,12 +34,14 @@ for f in glob.glob(os.path.join(root, "kt", "run_kernel_trace.csv")):
 c = dict(agg)
 # the probe runs one check per pass (PROBE_REPS=1); the trace's launches are that check's
 kt = sum(durs)
-fetch = c.get("FETCH_SIZE", 0.0) * 1024 * 2
+fscale = float(os.environ.get("PMC_FETCH_SCALE", "2"))
+fetch = c.get("FETCH_SIZE", 0.0) * 1024 * fscale
 write = c.get("WRITE_SIZE", 0.0) * 1024
 res = dict(case=case, kernels=sorted(names), launches=len(durs), kernel_s=kt, counters=c,
            fetch_bytes_corrected=fetch, write_bytes=write, hbm_bytes=fetch + write,
-           note="one counter group per rocprofv3 pass; FETCH_SIZE x 1024 x 2 (gfx950 tallies 128-B reads "
-                "at 64 B), WRITE_SIZE x 1024; SQ_*_CYCLES in quad-cycles; one complete check per pass")
+           note=f"one counter group per rocprofv3 pass; FETCH_SIZE x 1024 x {fscale:g} (x2: gfx950 tallies 128-B "
+                "streaming reads at 64 B; x1: scattered probes, one 64-B request each), WRITE_SIZE x 1024; "
+                "SQ_*_CYCLES in quad-cycles; one complete check per pass")
 if kt > 0 and c:
     t_valu = c.get("SQ_INSTS_VALU", 0) * 2 / (CUS * SIMDS * CLOCK_HZ)
     t_salu = c.get("SQ_INSTS_SALU", 0) / (CUS * CLOCK_HZ)

@@ -128,6 +128,68 @@ def test_run_node_error_counts_at_level_end(case, partition, ranks):
     assert r.transport == "local"  # ranks share the one GPU
 
 
+def check_behavior(m, want, trace):
+    """a shortest behavior of the spec ending in the golden case's error: an
+    initial state, one Next step per state (host_successors, the model.h
+    semantics the oracles pin), as long as TLC's trace, its last state
+    violating the reported invariant (or without a successor: deadlock)"""
+    assert len(trace) == len(want["trace"])
+    assert trace[0][0] == "Init"
+    assert trace[0][1] in {tlcgpu.host_init_state(m, i) for i in range(tlcgpu.init_count(m))}
+    for (_, s), (a, t) in zip(trace, trace[1:]):
+        assert (a, t) in tlcgpu.host_successors(m, s)
+    last = trace[-1][1]
+    if want["result"] == "invariant":
+        code = tlcgpu.host_check_invariants(m, last)
+        assert code >= 0 and m.invariants[code >> 1] == want["invariant"]
+        # and no shorter prefix violates
+        assert all(tlcgpu.host_check_invariants(m, s) < 0 for _, s in trace[:-1])
+    else:
+        assert want["result"] == "deadlock" and not tlcgpu.host_successors(m, last)
+
+
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+@pytest.mark.parametrize("case,partition", [("V_leak", 0), ("V_dup", 0), ("V_leak_producer", 0), ("V_dup_producer", 0),
+                                            ("V_leak", 2), ("V_dup", 2), ("D_N0_K1", 0), ("D_N0_K1", 2),
+                                            ("W_C12_leak", 0)])
+def test_run_node_trace_across_ranks(case, partition, ranks):
+    """the first error's counterexample walked across the ranks'
+    stores without a re-run (tlcg_run_node_trace; csrc/tlcgpu.hip
+    trace_ranks): with partition 2 and with the Producer the chain crosses
+    ranks, state by state, through the parent references that name them"""
+    want = GOLDEN[case]["result"]
+    m = model_of(GOLDEN[case]["constants"])
+    r = tlcgpu.run_node(m, ranks, partition=partition)
+    assert (r.status, r.depth) == (want["result"], want["depth"])
+    check_behavior(m, want, r.trace)
+
+
+def test_run_node_trace_empty_when_the_model_holds():
+    r = tlcgpu.run_node(model_of(GOLDEN["S"]["constants"]), 4, partition=2)
+    assert r.status == "ok" and r.trace == []
+
+
+@pytest.mark.parametrize("case", ["V_leak", "V_dup_producer"])
+def test_run_comm_trace_world1(case):
+    """tlcg_run_comm over the RCCL transport (world 1) leaves the walked
+    counterexample for tlcg_trace_words"""
+    import ctypes as C
+    want = GOLDEN[case]["result"]
+    m = model_of(GOLDEN[case]["constants"])
+    ck = tlcgpu.Checker(m)
+    try:
+        lib = ck.lib
+        buf = C.create_string_buffer(128)
+        assert lib.tlcg_comm_unique_id(buf, 128) == 128
+        assert lib.tlcg_comm_init(ck.ctx, buf, 128) == 0, lib.tlcg_last_error(ck.ctx)
+        st = tlcgpu.tlcg_stats()
+        assert lib.tlcg_run_comm(ck.ctx, C.byref(st), None, 0, None) == 0, lib.tlcg_last_error(ck.ctx)
+        assert tlcgpu.STATUS[st.status] == want["result"]
+        check_behavior(m, want, ck.trace())
+    finally:
+        ck.close()
+
+
 # SURVEY App.A.2: distinct states per BFS level of one initial message sequence
 PER_M_LEVELS = [1, 2, 2, 3, 3, 3, 4, 3, 3, 4, 4, 3, 4, 4, 4, 5, 5, 1, 2, 2]
 
