@@ -90,6 +90,11 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 #ifndef TLCG_LVL_UNIFORM
 #define TLCG_LVL_UNIFORM 0
 #endif
+// component codes: the invariants of both successors evaluated before their
+// FPSet probes, overlapping the LDS round trip (A/B)
+#ifndef TLCG_SPEC_INV
+#define TLCG_SPEC_INV 0
+#endif
 template <int K>
 struct CodeShape { static constexpr int T = (K * TLCG_CODE_FPSET_NUM / TLCG_CODE_FPSET_DEN + 15) / 16 * 16; };
 
@@ -222,7 +227,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     lvl_end = tail;
     // the insert of a new state: queue, HBM store + parent log; returns the
     // first failing invariant + 1 (0: all hold)
-    auto insert = [&](lkey key, int action, int pos) -> int {
+    auto insert = [&](lkey key, int action, int pos, int pinv = -1) -> int {
       Q(tail) = (qword)key;
 #ifndef TLCG_NO_STORE  // (experiment only: measures what the HBM store costs)
       if constexpr (CREC) {
@@ -239,6 +244,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
 #ifdef TLCG_NO_INV  // (experiment only: measures what the invariants cost)
       return 0;
 #else
+      if (TLCG_SPEC_INV && CODE) return pinv;  // (evaluated before the probe)
       if constexpr (CODE) return check_invariants_cb(L, ccon, key) + 1;
       else return check_invariants_k(L, cmsg, key) + 1;
 #endif
@@ -248,7 +254,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     // lookup, insert, invariants (TLC's FPSet.put + check).  (Flags the caller
     // owns are set by the caller: written through the lambda they ended up in
     // scratch memory, read back behind a vmcnt(0) wait on every expansion.)
-    auto visit = [&](lkey key, int action, int pos, unsigned sl, unsigned e) -> Visit {
+    auto visit = [&](lkey key, int action, int pos, unsigned sl, unsigned e, int pinv = -1) -> Visit {
 #ifndef TLCG_PROBE_LOOP_ONLY
       // the first slot outside the loop: most probes end there (an empty
       // slot, or the state itself), so the divergent loop's exec-mask
@@ -274,7 +280,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       if (tail >= K) return Visit{-2, 0};  // does not fit on chip: cascade
 #endif
       H(sl) = (uint8_t)(tail + 1);
-      return Visit{(int)sl | (insert(key, action, pos) << 16), 0};
+      return Visit{(int)sl | (insert(key, action, pos, pinv) << 16), 0};
     };
 #else
     // visit one successor whose probe starts at bucket `b` holding `w`: FPSet
@@ -373,6 +379,17 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       const unsigned sl1 = slot_of<T>(t, a.mult), sl2 = slot_of<T>(t2, a.mult);
       const unsigned e1 = H(sl1);  // (unconditional reads; unused when the action is disabled)
       unsigned e2 = H(sl2);
+#if TLCG_SPEC_INV
+      // both successors' invariants evaluated while their first slots are
+      // read (most successors are new; the rest evaluate them in vain)
+      int pinv1 = -1, pinv2 = -1;
+      if constexpr (CODE) {
+        pinv1 = check_invariants_cb(L, ccon, t) + 1;
+        pinv2 = check_invariants_cb(L, ccon, t2) + 1;
+      }
+#else
+      constexpr int pinv1 = -1, pinv2 = -1;
+#endif
 #else
       const unsigned sl1 = bucket_of<NB>(t), sl2 = bucket_of<NB>(t2);
       const uint32_t e1 = r == 1 ? hb[sl1][lane] : 0u;
@@ -382,7 +399,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       int ev1 = 0, ev2 = 0;  // FLAT: first failing invariant + 1 of an inserted successor
       if (r == 1) {
         ++nsucc;
-        const Visit v1 = visit(t, action, head, sl1, e1);
+        const Visit v1 = visit(t, action, head, sl1, e1, pinv1);
         const int ins = settle(v1, action, head);
         if (ins >= 0) first_new = t;
         ev1 = v1.code >= 0 ? v1.code >> 16 : 0;
@@ -394,7 +411,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       }
       if ((TLCG_COMP_FLAT || alive) && crash) {  // (FLAT: a lane in the loop is alive)
         ++nsucc;
-        const Visit v2 = visit(t2, ACT_CRASH, head, sl2, e2);
+        const Visit v2 = visit(t2, ACT_CRASH, head, sl2, e2, pinv2);
         const int ins = settle(v2, ACT_CRASH, head);
         if (ins >= 0 && tail0 == tail - 1) first_new = t2;
         ev2 = v2.code >= 0 ? v2.code >> 16 : 0;
