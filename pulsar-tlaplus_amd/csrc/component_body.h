@@ -91,9 +91,12 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 #define TLCG_LVL_UNIFORM 0
 #endif
 // component codes: the invariants of both successors evaluated before their
-// FPSet probes, overlapping the LDS round trip (A/B)
+// FPSet probes, so the VALU work overlaps the probes' LDS round trips (a
+// successor found seen evaluated them in vain: 1.34 evaluations per new
+// state instead of 1).  G9 4.84 -> 4.62 ms, M8 0.575 -> 0.546 ms
+// (profiles/r03_comp_spec_inv_ab.jsonl).  0: evaluated on insert, for A/B
 #ifndef TLCG_SPEC_INV
-#define TLCG_SPEC_INV 0
+#define TLCG_SPEC_INV 1
 #endif
 template <int K>
 struct CodeShape { static constexpr int T = (K * TLCG_CODE_FPSET_NUM / TLCG_CODE_FPSET_DEN + 15) / 16 * 16; };

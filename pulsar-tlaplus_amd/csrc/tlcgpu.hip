@@ -863,6 +863,7 @@ struct tlcg_ctx {
   u64 comp_generated = 0, comp_distinct = 0, comp_store_used = 0;
   unsigned long long* d_comp = nullptr;  // lvl[COMP_MAXLV], totals[2], event, ovf_n, outdeg[3], lvl_gen[COMP_MAXLV]
   unsigned long long* h_comp = nullptr;
+  bool comp_clean = false;  // d_comp holds zeros (and the event's ~0): k_comp_finish reset it
   u64* d_ovf[2] = {nullptr, nullptr};
   u64 ovf_cap = 0;
   // layout-specialized kernels (jit.cpp): 0 untried, 1 built, -1 failed (precompiled ones used)
@@ -1833,11 +1834,29 @@ bool component_applicable(const tlcg_ctx* c) {
          c->hm.n_init < (1ull << 36) && !c->hm.user;
 }
 
+// Fold the COMP_STRIPES copies of a pass's counters into out[0, kCompCounters)
+// (the event and the overflow count live in copy 0 only) and reset every copy
+// for the next pass, in stream order behind the pass: one small launch instead
+// of two memsets before the pass and a 53-KB copy and a host fold after it
+__global__ __launch_bounds__(128) void k_comp_finish(unsigned long long* __restrict__ ctr,
+                                                     unsigned long long* __restrict__ out) {
+  const int i = threadIdx.x;
+  if (i >= kCompCounters) return;
+  const bool single = i == COMP_MAXLV + 2 || i == COMP_MAXLV + 3;
+  unsigned long long s = ctr[i];
+  if (!single)
+    for (int k = 1; k < COMP_STRIPES; ++k) s += ctr[(size_t)k * kCompCounters + i];
+  out[i] = s;
+  for (int k = 0; k < COMP_STRIPES; ++k) ctr[(size_t)k * kCompCounters + i] = k == 0 && i == COMP_MAXLV + 2 ? ~0ull : 0ull;
+}
+
 bool comp_scratch(tlcg_ctx* c, u64 n) {
   if (!c->d_comp) {
-    const size_t bytes = sizeof(unsigned long long) * kCompCounters * COMP_STRIPES;
+    // the copies, then the folded counters (k_comp_finish)
+    const size_t bytes = sizeof(unsigned long long) * kCompCounters * (COMP_STRIPES + 1);
     if (!alloc_bytes(c, (void**)&c->d_comp, bytes, "component counters")) return false;
-    HIPCHK(hipHostMalloc((void**)&c->h_comp, bytes));
+    HIPCHK(hipHostMalloc((void**)&c->h_comp, sizeof(unsigned long long) * kCompCounters));
+    c->comp_clean = false;
   }
   if (n > c->ovf_cap) {
     hipFree(c->d_ovf[0]);
@@ -1912,8 +1931,11 @@ int run_component(tlcg_ctx* c) {
       HIPCHK_I(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
     }
     const int out = cur == 0 ? 1 : 0;
-    HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * kCompCounters * COMP_STRIPES, c->stream));
-    HIPCHK_I(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
+    if (!c->comp_clean) {  // (the first pass, or after a failed one; else k_comp_finish reset them)
+      HIPCHK_I(hipMemsetAsync(c->d_comp, 0, sizeof(unsigned long long) * kCompCounters * COMP_STRIPES, c->stream));
+      HIPCHK_I(hipMemsetAsync(c->d_comp + COMP_MAXLV + 2, 0xFF, sizeof(unsigned long long), c->stream));
+    }
+    c->comp_clean = false;
     CompArgs a;
     a.L = L;
     a.comp0 = r0;
@@ -1941,15 +1963,13 @@ int run_component(tlcg_ctx* c) {
       return -1;
     }
     HIPCHK_I(hipEventRecord(c->e1, c->stream));
-    HIPCHK_I(hipMemcpyAsync(c->h_comp, c->d_comp, sizeof(unsigned long long) * kCompCounters * COMP_STRIPES,
-                          hipMemcpyDeviceToHost, c->stream));
+    unsigned long long* const folded = c->d_comp + (size_t)kCompCounters * COMP_STRIPES;
+    k_comp_finish<<<1, 128, 0, c->stream>>>(c->d_comp, folded);
+    HIPCHK_I(hipGetLastError());
+    c->comp_clean = true;
+    HIPCHK_I(hipMemcpyAsync(c->h_comp, folded, sizeof(unsigned long long) * kCompCounters, hipMemcpyDeviceToHost,
+                            c->stream));
     HIPCHK_I(hipStreamSynchronize(c->stream));
-    // fold the stripes into copy 0 (the event and the overflow count live there only)
-    for (int sidx = 1; sidx < COMP_STRIPES; ++sidx) {
-      const unsigned long long* h = c->h_comp + (size_t)sidx * kCompCounters;
-      for (int i = 0; i < kCompCounters; ++i)
-        if (i != COMP_MAXLV + 2 && i != COMP_MAXLV + 3) c->h_comp[i] += h[i];
-    }
     float ms = 0;
     hipEventElapsedTime(&ms, c->e0, c->e1);
     c->kernel_ms += ms;

@@ -442,14 +442,15 @@ int main(int argc, char** argv) {
     }
     if (o.trace && (tctx || use_node_trace)) {
       const int words = state_words;  // 1, or 2 for a > 63-bit layout
-      std::vector<uint64_t> states((size_t)words << 16);
-      std::vector<int32_t> acts(1 << 16);
-      int32_t n = 0;
-      if (use_node_trace) {
-        states = node_states;
-        acts = node_acts;
-        n = std::min<int32_t>(node_tlen, (int32_t)acts.size());
+      std::vector<uint64_t> own_states;
+      std::vector<int32_t> own_acts;
+      if (!use_node_trace) {
+        own_states.resize((size_t)words << 16);
+        own_acts.resize(1 << 16);
       }
+      std::vector<uint64_t>& states = use_node_trace ? node_states : own_states;
+      std::vector<int32_t>& acts = use_node_trace ? node_acts : own_acts;
+      int32_t n = use_node_trace ? std::min<int32_t>(node_tlen, (int32_t)acts.size()) : 0;
       if (use_node_trace || tlcg_trace_words(tctx, states.data(), acts.data(), (int32_t)acts.size(), &n) == 0) {
         std::printf("Error: The behavior up to this point is:\n");
         std::vector<char> buf(1 << 16);
