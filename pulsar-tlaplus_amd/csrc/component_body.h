@@ -98,6 +98,11 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 #ifndef TLCG_SPEC_INV
 #define TLCG_SPEC_INV 1
 #endif
+// component codes: the queue entry behind the second successor's first FPSet
+// slot read before the first successor's probe (A/B)
+#ifndef TLCG_PREFETCH_Q2
+#define TLCG_PREFETCH_Q2 0
+#endif
 template <int K>
 struct CodeShape { static constexpr int T = (K * TLCG_CODE_FPSET_NUM / TLCG_CODE_FPSET_DEN + 15) / 16 * 16; };
 
@@ -257,13 +262,13 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     // lookup, insert, invariants (TLC's FPSet.put + check).  (Flags the caller
     // owns are set by the caller: written through the lambda they ended up in
     // scratch memory, read back behind a vmcnt(0) wait on every expansion.)
-    auto visit = [&](lkey key, int action, int pos, unsigned sl, unsigned e, int pinv = -1) -> Visit {
+    auto visit = [&](lkey key, int action, int pos, unsigned sl, unsigned e, int pinv = -1, int qpre = -1) -> Visit {
 #ifndef TLCG_PROBE_LOOP_ONLY
       // the first slot outside the loop: most probes end there (an empty
       // slot, or the state itself), so the divergent loop's exec-mask
       // bookkeeping is paid only on a collision
       if (e != 0) {
-        if (Q(e - 1) == key) return Visit{-1, 0};  // seen
+        if ((qpre >= 0 ? (lkey)qpre : (lkey)Q(e - 1)) == key) return Visit{-1, 0};  // seen
         for (int p = 1; p < T; ++p) {
           sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
           e = H(sl);
@@ -293,7 +298,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     // takes the state; a full bucket (rare at load <= 2/3) moves on to the
     // next.  (Flags the caller owns are set by the caller: written through
     // the lambda they ended up in scratch memory, read behind vmcnt(0).)
-    auto visit = [&](lkey key, int action, int pos, unsigned b, uint32_t w) -> Visit {
+    auto visit = [&](lkey key, int action, int pos, unsigned b, uint32_t w, int pinv = -1, int = -1) -> Visit {
       for (int step = 0; step < NB; ++step) {
         const unsigned e0 = w & 255u, e1 = (w >> 8) & 255u, e2 = (w >> 16) & 255u, e3 = w >> 24;
         const lkey q0 = Q(e0 ? e0 - 1 : 0), q1 = Q(e1 ? e1 - 1 : 0);
@@ -304,7 +309,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
           if (tail >= K) return Visit{-2, 0};  // does not fit on chip: cascade
           const uint32_t nw = w | ((uint32_t)(tail + 1) << (__builtin_ctz(z) & 24));
           hb[b][lane] = nw;
-          return Visit{(int)b | (insert(key, action, pos) << 16), nw};
+          return Visit{(int)b | (insert(key, action, pos, pinv) << 16), nw};
         }
         b = b + 1 == (unsigned)NB ? 0 : b + 1;
         w = hb[b][lane];
@@ -382,6 +387,11 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       const unsigned sl1 = slot_of<T>(t, a.mult), sl2 = slot_of<T>(t2, a.mult);
       const unsigned e1 = H(sl1);  // (unconditional reads; unused when the action is disabled)
       unsigned e2 = H(sl2);
+#else
+      const unsigned sl1 = bucket_of<NB>(t), sl2 = bucket_of<NB>(t2);
+      const uint32_t e1 = r == 1 ? hb[sl1][lane] : 0u;
+      uint32_t e2 = crash ? hb[sl2][lane] : 0u;
+#endif
 #if TLCG_SPEC_INV
       // both successors' invariants evaluated while their first slots are
       // read (most successors are new; the rest evaluate them in vain)
@@ -393,10 +403,12 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
 #else
       constexpr int pinv1 = -1, pinv2 = -1;
 #endif
+#if TLCG_PREFETCH_Q2 && !defined(TLCG_BUCKETS)
+      // the queue entry behind the second successor's first slot, read while
+      // the first successor probes (valid unless that one takes the slot)
+      int q2pre = (int)Q(e2 ? e2 - 1 : 0);
 #else
-      const unsigned sl1 = bucket_of<NB>(t), sl2 = bucket_of<NB>(t2);
-      const uint32_t e1 = r == 1 ? hb[sl1][lane] : 0u;
-      uint32_t e2 = crash ? hb[sl2][lane] : 0u;
+      int q2pre = -1;
 #endif
       lkey first_new = 0;
       int ev1 = 0, ev2 = 0;  // FLAT: first failing invariant + 1 of an inserted successor
@@ -407,14 +419,17 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
         if (ins >= 0) first_new = t;
         ev1 = v1.code >= 0 ? v1.code >> 16 : 0;
 #ifndef TLCG_BUCKETS
-        if (ins == (int)sl2 && crash) e2 = H(sl2);  // the slot just taken
+        if (ins == (int)sl2 && crash) {  // the slot just taken
+          e2 = H(sl2);
+          q2pre = -1;
+        }
 #else
         if (ins == (int)sl2) e2 = v1.nw;  // the bucket just written
 #endif
       }
       if ((TLCG_COMP_FLAT || alive) && crash) {  // (FLAT: a lane in the loop is alive)
         ++nsucc;
-        const Visit v2 = visit(t2, ACT_CRASH, head, sl2, e2, pinv2);
+        const Visit v2 = visit(t2, ACT_CRASH, head, sl2, e2, pinv2, q2pre);
         const int ins = settle(v2, ACT_CRASH, head);
         if (ins >= 0 && tail0 == tail - 1) first_new = t2;
         ev2 = v2.code >= 0 ? v2.code >> 16 : 0;
