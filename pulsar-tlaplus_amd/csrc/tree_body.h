@@ -35,6 +35,11 @@ namespace tlcg {
 #ifndef TLCG_TREE_CODE_STORE
 #define TLCG_TREE_CODE_STORE 1
 #endif
+// closed mode: a depth of at most half a group's lanes expands in one step
+// with one insert (pair mode, in the expansion loop); 0: two inserts, for A/B
+#ifndef TLCG_TREE_PAIR
+#define TLCG_TREE_PAIR 1
+#endif
 #ifndef TLCG_TREE_MULT  // the slot hash's multiplier (multiply-shift)
 #define TLCG_TREE_MULT 0x9E3779B1u
 #endif
@@ -268,8 +273,15 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     // expand depth d: compactor and BrokerCrash successors at depth d + 1
     u64 gen = 0;
     dbase = f1;  // depth d + 1 starts at f1
+    // pair mode (closed, TLCG_TREE_PAIR): a depth of at most S / 2 states
+    // runs in one step whose lanes j and j + S/2 both expand state j, the
+    // first inserting its compactor successor and the second its BrokerCrash
+    // one, so the depth takes one insert instead of two (the idle half of
+    // the group does the second); the store order is the same
+    const bool pairm = CLOSED && TLCG_TREE_PAIR && have && f1 - f0 <= S / 2;
+    const bool roleb = pairm && sub >= S / 2;  // (pair mode: this lane inserts the BrokerCrash successor)
     for (int b = f0; __ballot(have && b < f1); b += S) {
-      const int i = b + sub;
+      const int i = b + (pairm ? (sub & (S / 2 - 1)) : sub);
       const bool ok = have && i < f1;
       uint32_t k = 0;
       if constexpr (FB > 0) {
@@ -297,13 +309,16 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         crash = ok && crash_step_k(L, k, &t2);
         nsucc = nprod + (r == 1) + (int)crash + selfloop_count_k(L, cm, k);
       }
-      if (ok) {
+      if (ok && !roleb) {
         gen += (u64)nsucc;
         if (r == 2 || (nsucc == 0 && L.check_deadlock)) flags |= TREE_EVENT;
       }
       const u64 pref = (gb + (u64)i) << L.ord_bits;
-      insert(r == 1, t, pref | (u64)ordinal_of(L, act, 0), d + 1);
-      insert(crash, t2, pref | (u64)ordinal_of(L, ACT_CRASH, 0), d + 1);
+      // (one call for the whole wave: the insert ballots across the lanes)
+      insert(roleb ? crash : r == 1, roleb ? t2 : t,
+             pref | (u64)(roleb ? ordinal_of(L, ACT_CRASH, 0) : ordinal_of(L, act, 0)), d + 1);
+      const bool second = crash && !pairm;
+      if (!CLOSED || !TLCG_TREE_PAIR || __ballot(second)) insert(second, t2, pref | (u64)ordinal_of(L, ACT_CRASH, 0), d + 1);
     }
     // the group's sum of generated successors, added by its first lane
 #pragma unroll
