@@ -17,10 +17,14 @@ def r_c1(C):
     return 3 * C * C + 10 * C + 5
 
 
-@pytest.mark.parametrize("C", [16, 24, 32])
+@pytest.mark.parametrize("C", [12, 13, 14, 16, 24, 32])
 def test_compaction_times_limit_up_to_32(C):
     """CompactionTimesLimit up to the build's maximum (32): one initial state
-    (KeySpace = ValueSpace = {}, N = 1); C >= 24 are wide (two-word) layouts."""
+    (KeySpace = ValueSpace = {}, N = 1); C >= 24 are wide (two-word) layouts.
+    C = 12 / 13 / 14 put the one component at 557 / 642 / 733 states, around
+    the component tree's 640-state chunk: 642 fills the chunk's table within
+    its last depth, which must send the component on to the 2048-state pass
+    (ADVICE r2), not drop states."""
     m = tlcgpu.Model(msg_sent_limit=1, compaction_times_limit=C, key_space=[], value_space=[])
     r = tlcgpu.run(m)
     assert r.status == "ok"
