@@ -40,6 +40,9 @@ namespace tlcg {
 #ifndef TLCG_TREE_PAIR
 #define TLCG_TREE_PAIR 1
 #endif
+#ifndef TLCG_TREE_PAIR_OPEN  // (the same in Producer mode; A/B)
+#define TLCG_TREE_PAIR_OPEN 0
+#endif
 #ifndef TLCG_TREE_MULT  // the slot hash's multiplier (multiply-shift)
 #define TLCG_TREE_MULT 0x9E3779B1u
 #endif
@@ -278,7 +281,8 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     // first inserting its compactor successor and the second its BrokerCrash
     // one, so the depth takes one insert instead of two (the idle half of
     // the group does the second); the store order is the same
-    const bool pairm = CLOSED && TLCG_TREE_PAIR && have && f1 - f0 <= S / 2;
+    constexpr bool PAIR = CLOSED ? TLCG_TREE_PAIR : TLCG_TREE_PAIR_OPEN;
+    const bool pairm = PAIR && have && f1 - f0 <= S / 2;
     const bool roleb = pairm && sub >= S / 2;  // (pair mode: this lane inserts the BrokerCrash successor)
     for (int b = f0; __ballot(have && b < f1); b += S) {
       const int i = b + (pairm ? (sub & (S / 2 - 1)) : sub);
@@ -318,7 +322,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       insert(roleb ? crash : r == 1, roleb ? t2 : t,
              pref | (u64)(roleb ? ordinal_of(L, ACT_CRASH, 0) : ordinal_of(L, act, 0)), d + 1);
       const bool second = crash && !pairm;
-      if (!CLOSED || !TLCG_TREE_PAIR || __ballot(second)) insert(second, t2, pref | (u64)ordinal_of(L, ACT_CRASH, 0), d + 1);
+      if (!PAIR || __ballot(second)) insert(second, t2, pref | (u64)ordinal_of(L, ACT_CRASH, 0), d + 1);
     }
     // the group's sum of generated successors, added by its first lane
 #pragma unroll
