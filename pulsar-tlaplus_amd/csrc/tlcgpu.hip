@@ -864,6 +864,11 @@ struct tlcg_ctx {
   unsigned long long* d_comp = nullptr;  // lvl[COMP_MAXLV], totals[2], event, ovf_n, outdeg[3], lvl_gen[COMP_MAXLV]
   unsigned long long* h_comp = nullptr;
   bool comp_clean = false;  // d_comp holds zeros (and the event's ~0): k_comp_finish reset it
+  // the code pass's 32-bit records (comp_record), in their own buffer: global
+  // indices [0, slots) of that pass live here, and the state store's device
+  // window starts after them (win), so the store holds only the cascade passes
+  uint32_t* d_crec = nullptr;
+  u64 crec_cap = 0;
   u64* d_ovf[2] = {nullptr, nullptr};
   u64 ovf_cap = 0;
   // layout-specialized kernels (jit.cpp): 0 untried, 1 built, -1 failed (precompiled ones used)
@@ -1603,7 +1608,7 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   st->depth = depth;
   st->engine = (uint64_t)c->engine;
   st->jit_used = (c->jit_used ? 1 : 0) | (c->engine == TLCG_ENGINE_COMPONENT && c->comp_code ? 2 : 0);
-  st->host_states = c->win;
+  st->host_states = c->engine == TLCG_ENGINE_GLOBAL ? c->win : 0;  // (the component engine's window starts after its records)
   st->fpset_host_states = c->t0_base;
   if (std::getenv("TLCG_TIER_TRACE") && c->opts.fpset_spill)
     std::fprintf(stderr,
@@ -1669,8 +1674,7 @@ u64 comp_slot_decode(const tlcg_ctx* c, const tlcg_ctx::CompPass& ps, u64 g, uin
 bool state_at(tlcg_ctx* c, u64 g, u128* s, u64* p) {
   if (const tlcg_ctx::CompPass* ps = comp_code_pass(c, g)) {
     uint32_t rec = 0;
-    HIPCHK(hipMemcpy(&rec, reinterpret_cast<const uint32_t*>(c->d_states + ps->store_base) + (g - ps->store_base), 4,
-                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&rec, c->d_crec + (g - ps->store_base), 4, hipMemcpyDeviceToHost));
     *s = comp_slot_decode(c, *ps, g, rec, p);
     return true;
   }
@@ -1918,7 +1922,6 @@ int run_component(tlcg_ctx* c) {
     const int K = kCascade[p];
     const u64 base = c->comp_store_used;
     const u64 slots = component_store_slots(n, K);
-    if (!ensure_store(c, base + slots)) return -1;
     // the first pass runs component codes when they fit 16 bits (component_code.h);
     // a component whose initial key is no code, and the cascade, run 32-bit keys
     const bool code = p == 0 && K <= 64 && c->comp_code;
@@ -1926,6 +1929,18 @@ int run_component(tlcg_ctx* c) {
     // (its store holds records unless an A/B build of the specialized kernels asked for words)
     const char* jd = std::getenv("TLCG_JIT_DEFINES");
     pass.codes = code && !(c->jit_used && jd && std::strstr(jd, "TLCG_COMP_CODE_STORE=0"));
+    if (pass.codes) {
+      // 4 B per slot in the record buffer, none in the state store (16 B)
+      if (c->crec_cap < slots) {
+        hipFree(c->d_crec);
+        c->d_crec = nullptr;
+        c->crec_cap = 0;
+        if (!alloc_bytes(c, (void**)&c->d_crec, slots * 4, "component records")) return -1;
+        c->crec_cap = slots;
+      }
+    } else if (!ensure_store(c, base + slots)) {
+      return -1;
+    }
     if (cur >= 0) {
       pass.list.resize(n);
       HIPCHK_I(hipMemcpy(pass.list.data(), c->d_ovf[cur], n * 8, hipMemcpyDeviceToHost));
@@ -1941,8 +1956,13 @@ int run_component(tlcg_ctx* c) {
     a.comp0 = r0;
     a.n_comp = n;
     a.list = cur >= 0 ? c->d_ovf[cur] : nullptr;
-    a.store = c->d_states + base;
-    a.parents = c->d_parents + base;
+    if (pass.codes) {  // (the kernel writes records only; its word and parent pointers are not dereferenced)
+      a.store = reinterpret_cast<u64*>(c->d_crec);
+      a.parents = reinterpret_cast<u64*>(c->d_crec);
+    } else {
+      a.store = dev_state(c, base);
+      a.parents = dev_parent(c, base);
+    }
     a.store_base = base;
     a.msgs_bits = mb;
     a.rank_tag = (u64)c->opts.rank << 56;
@@ -1983,11 +2003,16 @@ int run_component(tlcg_ctx* c) {
     c->comp_distinct += c->h_comp[COMP_MAXLV + 1];
     best_ev = std::min<u64>(best_ev, c->h_comp[COMP_MAXLV + 2]);
     c->comp_store_used = base + slots;
+    if (pass.codes) c->win = base + slots;  // (the store's device window holds the passes after it)
     c->passes.push_back(std::move(pass));
     n = c->h_comp[COMP_MAXLV + 3];
     cur = out;
   }
-  if (n) return 0;  // components beyond 255 states / 48 levels: the global engine takes the model
+  if (n) {  // components beyond 255 states / 48 levels: the global engine (or the tree) takes the model
+    c->win = 0;
+    c->passes.clear();
+    return 0;
+  }
   while (!c->comp_levels.empty() && c->comp_levels.back() == 0) c->comp_levels.pop_back();
   if (best_ev != NO_EVENT) {
     if (!resolve_comp_event(c, best_ev)) return -1;
@@ -2746,6 +2771,7 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_uev);
   jit_release(&c->jit);
   hipFree(c->d_comp);
+  hipFree(c->d_crec);
   hipFree(c->d_tree_dep);
   hipFree(c->d_tree_n);
   hipFree(c->d_tree_ctr);
@@ -2891,8 +2917,7 @@ int tlcg_copy_states_words(tlcg_ctx* c, uint64_t first, uint64_t n, uint64_t* ou
       if (const tlcg_ctx::CompPass* ps = comp_code_pass(c, first)) {
         m = std::min<u64>(n, ps->store_base + component_store_slots(ps->n, ps->K) - first);
         std::vector<uint32_t> rec(m);
-        if (hipMemcpy(rec.data(), reinterpret_cast<const uint32_t*>(c->d_states + ps->store_base) + (first - ps->store_base),
-                      m * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        if (hipMemcpy(rec.data(), c->d_crec + (first - ps->store_base), m * 4, hipMemcpyDeviceToHost) != hipSuccess) {
           c->err = "copy failed";
           return -10;
         }
