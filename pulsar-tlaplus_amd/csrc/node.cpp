@@ -52,23 +52,37 @@ extern "C" int tlcg_run_node_trace(const tlcg_model* m, const tlcg_opts* base, i
   }
   const int ndev = std::max(1, tlcg_device_count());
   std::vector<tlcg_ctx*> ctxs((size_t)n, nullptr);
+  // the contexts are created and destroyed by one thread per rank (their
+  // device allocations and FPSet clears overlap; one after the other they
+  // were a third of an 8-rank check's wall on one GPU)
   auto destroy_all = [&] {
-    for (auto* c : ctxs) tlcg_destroy(c);
+    std::vector<std::thread> dt;
+    for (auto* c : ctxs)
+      if (c) dt.emplace_back([c] { tlcg_destroy(c); });
+    for (auto& t : dt) t.join();
   };
   tlcg_peer_access(std::min(n, ndev));
-  for (int r = 0; r < n; ++r) {
-    tlcg_opts o = *base;
-    o.device = r % ndev;  // more ranks than devices: ranks share a device
-    o.rank = r;
-    o.world = n;
-    const int c = tlcg_create(m, &o, &ctxs[(size_t)r]);
-    if (c) {
+  std::vector<int> crc((size_t)n, 0);
+  {
+    std::vector<std::thread> ct;
+    for (int r = 0; r < n; ++r)
+      ct.emplace_back([&, r] {
+        tlcg_opts o = *base;
+        o.device = r % ndev;  // more ranks than devices: ranks share a device
+        o.rank = r;
+        o.world = n;
+        crc[(size_t)r] = tlcg_create(m, &o, &ctxs[(size_t)r]);
+      });
+    for (auto& t : ct) t.join();
+  }
+  for (int r = 0; r < n; ++r)
+    if (crc[(size_t)r]) {
       put_err(err, err_cap, "tlcg_create (rank " + std::to_string(r) + "): " +
                                 (ctxs[(size_t)r] ? tlcg_last_error(ctxs[(size_t)r]) : "no context"));
+      const int c = crc[(size_t)r];
       destroy_all();
       return c < 0 ? c : -1;
     }
-  }
   const char* force = std::getenv("TLCG_NODE_TRANSPORT");
   std::string why = n > ndev ? "more ranks than devices" : "TLCG_NODE_TRANSPORT=local";
   bool rccl = n <= ndev && !(force && !std::strcmp(force, "local")) && tlcg::rccl_available(&why);
