@@ -52,9 +52,9 @@ extern "C" int tlcg_run_node_trace(const tlcg_model* m, const tlcg_opts* base, i
   }
   const int ndev = std::max(1, tlcg_device_count());
   std::vector<tlcg_ctx*> ctxs((size_t)n, nullptr);
-  // the contexts are created and destroyed by one thread per rank (their
-  // device allocations and FPSet clears overlap; one after the other they
-  // were a third of an 8-rank check's wall on one GPU)
+  // the contexts are created and destroyed by one thread per rank, so the
+  // ranks' devices allocate and clear their stores and FPSets at once (ranks
+  // sharing one GPU serialize there anyway)
   auto destroy_all = [&] {
     std::vector<std::thread> dt;
     for (auto* c : ctxs)
