@@ -43,6 +43,11 @@ namespace tlcg {
 #ifndef TLCG_TREE_PAIR_OPEN  // (the same in Producer mode; A/B)
 #define TLCG_TREE_PAIR_OPEN 0
 #endif
+// a group of 16 lanes sums its generated successors per depth by a DPP row
+// scan (four VALU ops) instead of four ds_bpermute round trips; 0: shuffles, for A/B
+#ifndef TLCG_TREE_DPP
+#define TLCG_TREE_DPP 1
+#endif
 #ifndef TLCG_TREE_MULT  // the slot hash's multiplier (multiply-shift)
 #define TLCG_TREE_MULT 0x9E3779B1u
 #endif
@@ -274,7 +279,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     __syncthreads();
     const int f1 = n;  // depth d = [f0, f1)
     // expand depth d: compactor and BrokerCrash successors at depth d + 1
-    u64 gen = 0;
+    unsigned gen = 0;  // (a group's depth generates far fewer than 2^32 successors)
     dbase = f1;  // depth d + 1 starts at f1
     // pair mode (closed, TLCG_TREE_PAIR): a depth of at most S / 2 states
     // runs in one step whose lanes j and j + S/2 both expand state j, the
@@ -314,7 +319,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         nsucc = nprod + (r == 1) + (int)crash + selfloop_count_k(L, cm, k);
       }
       if (ok && !roleb) {
-        gen += (u64)nsucc;
+        gen += (unsigned)nsucc;
         if (r == 2 || (nsucc == 0 && L.check_deadlock)) flags |= TREE_EVENT;
       }
       const u64 pref = (gb + (u64)i) << L.ord_bits;
@@ -324,10 +329,18 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       const bool second = crash && !pairm;
       if (!PAIR || __ballot(second)) insert(second, t2, pref | (u64)ordinal_of(L, ACT_CRASH, 0), d + 1);
     }
-    // the group's sum of generated successors, added by its first lane
+    // the group's sum of generated successors, added by its last lane
+    if constexpr (S == 16 && TLCG_TREE_DPP) {
+      // inclusive scan inside the 16-lane row: lane 15 ends with the sum
+      gen += (unsigned)__builtin_amdgcn_update_dpp(0, (int)gen, 0x111, 0xf, 0xf, true);  // row_shr:1
+      gen += (unsigned)__builtin_amdgcn_update_dpp(0, (int)gen, 0x112, 0xf, 0xf, true);  // row_shr:2
+      gen += (unsigned)__builtin_amdgcn_update_dpp(0, (int)gen, 0x114, 0xf, 0xf, true);  // row_shr:4
+      gen += (unsigned)__builtin_amdgcn_update_dpp(0, (int)gen, 0x118, 0xf, 0xf, true);  // row_shr:8
+    } else {
 #pragma unroll
-    for (int off = S / 2; off > 0; off >>= 1) gen += __shfl_xor(gen, off);
-    if (have && sub == 0 && d < TREE_MAXLV && a.count) {
+      for (int off = S / 2; off > 0; off >>= 1) gen += __shfl_xor(gen, off);
+    }
+    if (have && sub == S - 1 && d < TREE_MAXLV && a.count) {
       atomicAdd(&lvl_d[d], (lvl_t)(f1 - f0));
       atomicAdd(&lvl_g[d], (lvl_t)gen);
     }
