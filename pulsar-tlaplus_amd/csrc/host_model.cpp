@@ -136,40 +136,54 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
   return true;
 }
 
+namespace {
+// the insert calls of component 0's BFS, in the kernels' order: per depth,
+// chunks of `group` states; per chunk the compactor successors, then
+// BrokerCrash's; and its codes in BFS order.  False when the component does
+// not fit T slots.
+bool comp0_calls(const HostModel& hm, int T, int group, std::vector<std::vector<uint32_t>>* calls,
+                 std::vector<uint32_t>* codes) {
+  const Layout& L = hm.L;
+  const u128 s0 = init_state<u128>(L, 0);
+  const CompMsgs cm = comp_msgs_init(L, (u64)s0);
+  const CodeConsts kc = code_consts(L, cm);
+  *calls = {{code_encode_w<u128>(L, s0)}};
+  *codes = {(*calls)[0][0]};
+  std::unordered_set<uint32_t> seen{(*calls)[0][0]};
+  std::vector<uint32_t> level{(*calls)[0][0]};
+  while (!level.empty() && seen.size() < (size_t)T) {
+    std::vector<uint32_t> next;
+    for (size_t b = 0; b < level.size(); b += (size_t)group) {
+      std::vector<uint32_t> c1, c2;
+      for (size_t i = b; i < b + (size_t)group && i < level.size(); ++i) {
+        ckey t = 0, t2 = 0;
+        int act = 0;
+        if (compactor_step_cb(L, kc, level[i], &t, &act) == 1) c1.push_back(t);
+        if (crash_step_c(L, level[i], &t2)) c2.push_back(t2);
+      }
+      for (auto* c : {&c1, &c2}) {
+        if (c->empty()) continue;
+        calls->push_back(*c);
+        for (uint32_t k : *c)
+          if (seen.insert(k).second) {
+            next.push_back(k);
+            codes->push_back(k);
+          }
+      }
+    }
+    level.swap(next);
+  }
+  return seen.size() < (size_t)T;
+}
+}  // namespace
+
 uint32_t tune_slot_mult(const HostModel& hm, int T, int group, int candidates) {
   const Layout& L = hm.L;
   const uint32_t def = 0x9E3779B1u;
   if (L.producer || T <= 0 || group <= 0) return def;
-  // the insert calls of component 0's BFS, in the kernels' order: per depth,
-  // chunks of `group` states; per chunk the compactor successors, then BrokerCrash's
-  const u128 s0 = init_state<u128>(L, 0);
-  const CompMsgs cm = comp_msgs_init(L, (u64)s0);
-  const CodeConsts kc = code_consts(L, cm);
-  std::vector<std::vector<uint32_t>> calls{{code_encode_w<u128>(L, s0)}};
-  {
-    std::unordered_set<uint32_t> seen{calls[0][0]};
-    std::vector<uint32_t> level{calls[0][0]};
-    while (!level.empty() && seen.size() < (size_t)T) {
-      std::vector<uint32_t> next;
-      for (size_t b = 0; b < level.size(); b += (size_t)group) {
-        std::vector<uint32_t> c1, c2;
-        for (size_t i = b; i < b + (size_t)group && i < level.size(); ++i) {
-          ckey t = 0, t2 = 0;
-          int act = 0;
-          if (compactor_step_cb(L, kc, level[i], &t, &act) == 1) c1.push_back(t);
-          if (crash_step_c(L, level[i], &t2)) c2.push_back(t2);
-        }
-        for (auto* c : {&c1, &c2}) {
-          if (c->empty()) continue;
-          calls.push_back(*c);
-          for (uint32_t k : *c)
-            if (seen.insert(k).second) next.push_back(k);
-        }
-      }
-      level.swap(next);
-    }
-    if (seen.size() >= (size_t)T) return def;  // does not fit the table: nothing to tune
-  }
+  std::vector<std::vector<uint32_t>> calls;
+  std::vector<uint32_t> codes;
+  if (!comp0_calls(hm, T, group, &calls, &codes)) return def;  // does not fit the table: nothing to tune
   auto trips = [&](uint32_t mult) {
     std::vector<uint32_t> h((size_t)T, 0);
     long total = 0;
@@ -207,6 +221,54 @@ uint32_t tune_slot_mult(const HostModel& hm, int T, int group, int candidates) {
     }
   }
   return best;
+}
+
+bool build_slot_disp(const HostModel& hm, int T, uint32_t mult, uint32_t* dmult, uint16_t* disp) {
+  constexpr int NB = 256;
+  std::fill(disp, disp + NB, (uint16_t)0);
+  *dmult = 0x85EBCA6Bu;
+  if (hm.L.producer || T <= 0 || T > 65535) return false;
+  std::vector<std::vector<uint32_t>> calls;
+  std::vector<uint32_t> codes;
+  if (!comp0_calls(hm, T, 16, &calls, &codes)) return false;
+  auto base = [&](uint32_t k) { return (unsigned)(((unsigned long long)(k * mult) * (unsigned)T) >> 32); };
+  uint64_t x = 0x2545F4914F6CDD1Dull;  // a fixed sequence: the choice is deterministic
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    const uint32_t dm = attempt == 0 ? *dmult : (uint32_t)((x ^= x << 13, x ^= x >> 7, x ^= x << 17) >> 16) | 1u;
+    std::vector<std::vector<uint32_t>> bucket(NB);
+    for (uint32_t k : codes) bucket[(k * dm) >> 24].push_back(k);
+    std::vector<int> order(NB);
+    for (int b = 0; b < NB; ++b) order[b] = b;
+    std::stable_sort(order.begin(), order.end(), [&](int p, int q) { return bucket[p].size() > bucket[q].size(); });
+    std::vector<char> used((size_t)T, 0);
+    uint16_t d[NB] = {};
+    bool ok = true;
+    for (int b : order) {
+      if (bucket[b].empty()) break;
+      int found = -1;
+      for (int dv = 0; dv < T && found < 0; ++dv) {
+        bool fits = true;
+        for (size_t i = 0; i < bucket[b].size() && fits; ++i) {
+          const unsigned s = (base(bucket[b][i]) + (unsigned)dv) % (unsigned)T;
+          fits = !used[s];
+          for (size_t j = 0; j < i && fits; ++j) fits = (base(bucket[b][j]) + (unsigned)dv) % (unsigned)T != s;
+        }
+        if (fits) found = dv;
+      }
+      if (found < 0) {
+        ok = false;
+        break;
+      }
+      d[b] = (uint16_t)found;
+      for (uint32_t k : bucket[b]) used[(base(k) + (unsigned)found) % (unsigned)T] = 1;
+    }
+    if (ok) {
+      *dmult = dm;
+      std::copy(d, d + NB, disp);
+      return true;
+    }
+  }
+  return false;
 }
 
 template <typename W>

@@ -37,6 +37,16 @@ std::vector<std::string> user_def_names(const char* text);
 // engine per component; 16: a component of the tree's closed mode).
 uint32_t tune_slot_mult(const HostModel& hm, int T, int group, int candidates);
 
+// the tree's closed mode: a displacement per bucket of component 0's codes
+// (bucket (code * *dmult) >> 24, TREE_DISP = 256 buckets), chosen so that
+// slot(code) = (multiply-shift slot of `mult` + disp[bucket]) mod T places
+// every code of the component in a slot of its own -- a perfect hash for the
+// code set every component shares without a Producer, so each insert finds
+// its slot at the first probe.  Linear probing stays behind it: the FPSet is
+// exact for any table (all zero: the plain multiply-shift slot).  False when
+// no table was found (then `disp` is all zero).
+bool build_slot_disp(const HostModel& hm, int T, uint32_t mult, uint32_t* dmult, uint16_t* disp);
+
 // every invariant of the cfg, the user's included: -1, else (index << 1) | is_error
 template <typename W>
 int host_check_all(const HostModel& hm, W s) {

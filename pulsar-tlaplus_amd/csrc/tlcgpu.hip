@@ -780,6 +780,8 @@ struct tlcg_ctx {
   HostModel hm;
   std::string user_defs;                 // model.user_defs points here (tlcg_create copies the caller's text)
   uint32_t comp_mult = 0, tree_mult = 0;  // tuned slot-hash multipliers (0: not yet)
+  uint32_t tree_disp_mult = 0;               // the tree's closed-mode slot displacements (build_slot_disp)
+  uint16_t tree_disp[TREE_DISP] = {};
   bool no_tree = false;                   // the ranks fell back from the sharded component tree (run_ranks)
   bool tree_codes = false;                // the store holds the tree's closed-mode component codes (tree_body.h)
   u64 tree_r0 = 0;                        //   of the components of initial states tree_r0, tree_r0 + 1, ..
@@ -2135,6 +2137,8 @@ int run_tree(tlcg_ctx* c) {
   if (closed && !c->tree_mult) {  // (640-slot tables, 16 lanes per component; tree_body.h)
     const char* tv = std::getenv("TLCG_TUNE_MULT");
     c->tree_mult = tv && std::atoi(tv) == 0 ? DEFAULT_SLOT_MULT : tune_slot_mult(c->hm, 640, 16, 4096);
+    // (zero displacements when none is found: the plain multiply-shift slot)
+    build_slot_disp(c->hm, 640, c->tree_mult, &c->tree_disp_mult, c->tree_disp);
   }
   for (int cap : closed ? std::vector<int>{640, 2048} : std::vector<int>{384, 1024}) {
     const u64 slots = comps * (u64)cap;
@@ -2193,6 +2197,8 @@ int run_tree(tlcg_ctx* c) {
       a.stripe = 2 * TREE_MAXLV;
       a.nstripe = TREE_STRIPES;
       a.mult = closed ? c->tree_mult : DEFAULT_SLOT_MULT;
+      a.disp_mult = c->tree_disp_mult;
+      std::copy(c->tree_disp, c->tree_disp + TREE_DISP, a.disp);  // (zeros unless closed)
       const bool jit = c->jit_used && (cap == 384 || cap == 1024 || cap == 640 || cap == 2048);
       const int g = cap == 384 || cap == 640 ? groups : 1;
       if (!(jit ? jit_launch_tree(c->jit, a, cap, c->stream) : launch_tree(a, cap, g, closed, words, c->stream))) {
