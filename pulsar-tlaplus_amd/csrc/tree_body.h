@@ -55,6 +55,9 @@ namespace tlcg {
 #ifndef TLCG_TREE_DISP
 #define TLCG_TREE_DISP 1
 #endif
+#ifndef TLCG_TREE_CAS1  // closed mode: the first CAS outside the probe loop; 0: inside (A/B)
+#define TLCG_TREE_CAS1 1
+#endif
 #ifndef TLCG_TREE_MULT  // the slot hash's multiplier (multiply-shift)
 #define TLCG_TREE_MULT 0x9E3779B1u
 #endif
@@ -159,7 +162,16 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         s += dsp[(key * a.disp_mult) >> 24];
         s = s >= (unsigned)TT ? s - (unsigned)TT : s;
       }
-      for (int p = 0; p < TT; ++p) {
+      int p0 = 0;
+      if constexpr (CLOSED && TLCG_TREE_CAS1) {
+        // the first CAS outside the probe loop: with the perfect hash it
+        // settles every insert, so the loop is skipped (no lane collides)
+        const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
+        isnew = old == 0;
+        p0 = old == 0 || old == key + 1u ? TT : 1;
+        s = s + 1 == (unsigned)TT ? 0u : s + 1;
+      }
+      for (int p = p0; p < TT; ++p) {
         const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
         // Producer mode: the probe loop with one exit (P8 2.07 -> 1.99 ms);
         // closed mode: two (G9-deep 31.7 vs 32.5 ms with one;
