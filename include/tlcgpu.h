@@ -261,6 +261,14 @@ int tlcg_host_check_invariants_batch(const tlcg_model* m, const uint64_t* states
  * only.  Returns the states compared (0: the component engine does not take
  * this model), or < 0 on a disagreement. */
 int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint64_t n);
+/* The component tree's closed-mode FPSet on the component of initial state
+ * `comp`, replayed on the host with the engine's slot hash (the tuned
+ * multiplier and the perfect-hash displacement table built from component
+ * 0): out[0] = insert calls, out[1] = probe trips (each call's longest lane)
+ * with the table, out[2] = without it; out[1] == out[0] when every insert
+ * takes one CAS.  Host only: 0, -1 when the closed tree does not take the
+ * component, -2 on a bad model. */
+int tlcg_host_tree_slot_probes(const tlcg_model* m, uint64_t comp, int64_t* out);
 /* PROPERTY Termination (compaction.tla:303-307).  Spec has no fairness, so a
  * behavior may stutter forever in its initial state: <>P fails iff an
  * initial state violates P.  Returns the first such initial state (TLC Init

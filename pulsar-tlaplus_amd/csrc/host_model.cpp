@@ -137,14 +137,15 @@ bool build_model(const tlcg_model& m, HostModel* out, std::string* err) {
 }
 
 namespace {
-// the insert calls of component 0's BFS, in the kernels' order: per depth,
-// chunks of `group` states; per chunk the compactor successors, then
-// BrokerCrash's; and its codes in BFS order.  False when the component does
-// not fit T slots.
-bool comp0_calls(const HostModel& hm, int T, int group, std::vector<std::vector<uint32_t>>* calls,
-                 std::vector<uint32_t>* codes) {
+// the insert calls of component `comp`'s BFS (the closure of initial state
+// comp), in the kernels' order: per depth, chunks of `group` states; per
+// chunk the compactor successors, then BrokerCrash's (`pair`: a depth of at
+// most group / 2 states in one call, the tree's pair mode); and its codes in
+// BFS order.  False when the component does not fit T slots.
+bool comp_calls(const HostModel& hm, int T, int group, u64 comp, bool pair, std::vector<std::vector<uint32_t>>* calls,
+                std::vector<uint32_t>* codes) {
   const Layout& L = hm.L;
-  const u128 s0 = init_state<u128>(L, 0);
+  const u128 s0 = init_state<u128>(L, comp);
   const CompMsgs cm = comp_msgs_init(L, (u64)s0);
   const CodeConsts kc = code_consts(L, cm);
   *calls = {{code_encode_w<u128>(L, s0)}};
@@ -161,6 +162,10 @@ bool comp0_calls(const HostModel& hm, int T, int group, std::vector<std::vector<
         if (compactor_step_cb(L, kc, level[i], &t, &act) == 1) c1.push_back(t);
         if (crash_step_c(L, level[i], &t2)) c2.push_back(t2);
       }
+      if (pair && level.size() <= (size_t)group / 2) {
+        c1.insert(c1.end(), c2.begin(), c2.end());
+        c2.clear();
+      }
       for (auto* c : {&c1, &c2}) {
         if (c->empty()) continue;
         calls->push_back(*c);
@@ -174,6 +179,40 @@ bool comp0_calls(const HostModel& hm, int T, int group, std::vector<std::vector<
     level.swap(next);
   }
   return seen.size() < (size_t)T;
+}
+bool comp0_calls(const HostModel& hm, int T, int group, std::vector<std::vector<uint32_t>>* calls,
+                 std::vector<uint32_t>* codes) {
+  return comp_calls(hm, T, group, 0, false, calls, codes);
+}
+// the probe trips of a group's longest lane, summed over the insert calls, on
+// a T-slot table probed linearly from the multiply-shift slot of `mult` plus
+// disp[(code * dmult) >> 24] (the tree kernel's insert, tree_body.h)
+long sim_trips(const std::vector<std::vector<uint32_t>>& calls, int T, uint32_t mult, uint32_t dmult,
+               const uint16_t* disp) {
+  std::vector<uint32_t> h((size_t)T, 0);
+  long total = 0;
+  for (const auto& c : calls) {
+    int longest = 0;
+    for (uint32_t key : c) {
+      unsigned sl = (unsigned)(((unsigned long long)(key * mult) * (unsigned)T) >> 32);
+      if (disp) {
+        sl += disp[(key * dmult) >> 24];
+        sl = sl >= (unsigned)T ? sl - (unsigned)T : sl;
+      }
+      int p = 1;
+      for (; p <= T; ++p) {
+        if (h[sl] == 0) {
+          h[sl] = key + 1;
+          break;
+        }
+        if (h[sl] == key + 1) break;
+        sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
+      }
+      longest = std::max(longest, p);
+    }
+    total += longest;
+  }
+  return total;
 }
 }  // namespace
 
@@ -566,6 +605,31 @@ int64_t tlcg_host_termination_counterexample(const tlcg_model* m) {
 // to itself (the two-valued fields the code relies on), and the code
 // evaluators must decode to the same successors and results.  Returns the states compared, or
 // -(1 + index of the first disagreeing state) on a mismatch.
+// The tree's closed-mode FPSet on component `comp`, replayed on the host
+// with the engine's tuned multiplier and displacement table (built from
+// component 0): out[0] = insert calls (16-lane groups, pair mode), out[1] =
+// probe trips of each call's longest lane with the table, out[2] = without
+// it.  0; -1 when the closed tree does not take the component (Producer
+// modelled, or more than 640 states); -2 on a bad model.
+int tlcg_host_tree_slot_probes(const tlcg_model* m, uint64_t comp, int64_t* out) {
+  HostModel hm;
+  std::string e;
+  if (!m || !out || !build_model(*m, &hm, &e)) return -2;
+  if (hm.L.producer || comp >= hm.n_init) return -1;
+  constexpr int T = 640;  // (the closed tree's first pass, tlcgpu.hip)
+  std::vector<std::vector<uint32_t>> calls;
+  std::vector<uint32_t> codes;
+  if (!comp_calls(hm, T, 16, comp, true, &calls, &codes)) return -1;
+  const uint32_t mult = tune_slot_mult(hm, T, 16, 4096);
+  uint32_t dmult = 0;
+  uint16_t disp[256];  // (TREE_DISP buckets, tree.h)
+  build_slot_disp(hm, T, mult, &dmult, disp);
+  out[0] = (int64_t)calls.size();
+  out[1] = sim_trips(calls, T, mult, dmult, disp);
+  out[2] = sim_trips(calls, T, mult, 0, nullptr);
+  return 0;
+}
+
 int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint64_t n) {
   HostModel hm;
   std::string e;

@@ -106,6 +106,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_host_successors": (C.c_int, [M, U64, C.POINTER(U64), C.POINTER(I32), I32]),
         "tlcg_host_check_invariants": (C.c_int, [M, U64]),
         "tlcg_host_component_selfcheck": (C.c_int64, [M, U64, U64]),
+        "tlcg_host_tree_slot_probes": (C.c_int, [M, U64, C.POINTER(C.c_int64)]),
         "tlcg_host_termination_counterexample": (C.c_int64, [M]),
         "tlcg_owner": (C.c_int, [P, U64]),
         "tlcg_expand": (C.c_int, [P, S]),
@@ -302,6 +303,18 @@ def host_component_selfcheck(model: Model, first: int, n: int) -> int:
     compared with the generic ones (< 0: a disagreement)."""
     m = model.to_c()
     return load_library().tlcg_host_component_selfcheck(C.byref(m), C.c_uint64(first), C.c_uint64(n))
+
+
+def host_tree_slot_probes(model: Model, comp: int):
+    """(insert calls, probe trips with the displacement table, without it) of
+    the closed tree's FPSet on component `comp`, replayed on the host; None
+    when the closed tree does not take it."""
+    m = model.to_c()
+    out = (C.c_int64 * 3)()
+    r = load_library().tlcg_host_tree_slot_probes(C.byref(m), C.c_uint64(comp), out)
+    if r == -2:
+        raise ValueError("bad model")
+    return None if r < 0 else (out[0], out[1], out[2])
 
 
 def host_check_invariants_batch(model: Model, states: Sequence[int]) -> List[int]:
