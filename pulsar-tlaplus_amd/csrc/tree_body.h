@@ -55,6 +55,15 @@ namespace tlcg {
 #ifndef TLCG_TREE_DISP
 #define TLCG_TREE_DISP 1
 #endif
+// closed mode: a state's invariants are evaluated when it is expanded (one
+// evaluation per expansion step, the depth's states spread over the group's
+// lanes) instead of when it is inserted (one per insert call, two per step
+// outside pair mode); every state is expanded once, at the depth after its
+// own, so the same states are checked and a violation still raises
+// TREE_EVENT (the global engine reports it); 0: at insert, for A/B
+#ifndef TLCG_TREE_INV_AT_EXPAND
+#define TLCG_TREE_INV_AT_EXPAND 1
+#endif
 #ifndef TLCG_TREE_CAS1  // closed mode: the first CAS outside the probe loop; 0: inside (A/B)
 #define TLCG_TREE_CAS1 1
 #endif
@@ -216,7 +225,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         else st[pos] = code_word<W>(L, kc, msgs, key);
 #endif
 #ifndef TLCG_TREE_NO_INV  // (experiment only: what the invariants cost)
-        if (check_invariants_cb(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
+        if (!TLCG_TREE_INV_AT_EXPAND && check_invariants_cb(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
 #endif
       } else {
         st[pos] = msgs | ((u64)key << mb);
@@ -338,6 +347,9 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       int act = 0, r, nsucc;
       bool crash;
       if constexpr (CLOSED) {
+#ifndef TLCG_TREE_NO_INV
+        if (TLCG_TREE_INV_AT_EXPAND && ok && check_invariants_cb(L, kc, k) >= 0) flags |= TREE_EVENT;
+#endif
         r = ok ? compactor_step_cb(L, kc, k, &t, &act) : 0;
         crash = ok && crash_step_c(L, k, &t2);
         nsucc = (r == 1) + (int)crash + selfloop_count_c(L, kc, k);
