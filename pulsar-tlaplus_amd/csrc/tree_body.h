@@ -61,8 +61,12 @@ namespace tlcg {
 // outside pair mode); every state is expanded once, at the depth after its
 // own, so the same states are checked and a violation still raises
 // TREE_EVENT (the global engine reports it); 0: at insert, for A/B
+// (_OPEN: Producer mode, where a component's entries are expanded too)
 #ifndef TLCG_TREE_INV_AT_EXPAND
 #define TLCG_TREE_INV_AT_EXPAND 1
+#endif
+#ifndef TLCG_TREE_INV_AT_EXPAND_OPEN  // (the same in Producer mode)
+#define TLCG_TREE_INV_AT_EXPAND_OPEN 1
 #endif
 #ifndef TLCG_TREE_CAS1  // closed mode: the first CAS outside the probe loop; 0: inside (A/B)
 #define TLCG_TREE_CAS1 1
@@ -230,7 +234,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       } else {
         st[pos] = msgs | ((u64)key << mb);
         dp[pos] = (uint8_t)dd;  // (read by the next layer)
-        if (check_invariants_k(L, cm, key) >= 0) flags |= TREE_EVENT;
+        if (!TLCG_TREE_INV_AT_EXPAND_OPEN && check_invariants_k(L, cm, key) >= 0) flags |= TREE_EVENT;
       }
     }
     n = n + cnt > CAP ? CAP : n + cnt;
@@ -354,6 +358,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         crash = ok && crash_step_c(L, k, &t2);
         nsucc = (r == 1) + (int)crash + selfloop_count_c(L, kc, k);
       } else {
+        if (TLCG_TREE_INV_AT_EXPAND_OPEN && ok && check_invariants_k(L, cm, k) >= 0) flags |= TREE_EVENT;
         r = ok ? compactor_step_k(L, cm, (u64)msgs, k, k_phase(L, k), &t, &act) : 0;
         crash = ok && crash_step_k(L, k, &t2);
         nsucc = nprod + (r == 1) + (int)crash + selfloop_count_k(L, cm, k);
