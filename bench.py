@@ -33,6 +33,36 @@ CONFIGS = {
     # an open state space: the producer modelled (the component tree on one
     # GPU; at N > 1 every level crosses ranks), oracle-pinned in tests/golden/p8.json
     "p8": dict(keys=7, producer=True, retain=False, distinct=91_781_506, generated=161_341_378, depth=23),
+    # BASELINE config 5 at scale: G9 with an invariant the user adds to the
+    # module (it holds, so the whole space is checked): the cfg's two spec
+    # invariants plus LatestIsLast, compiled from its TLA+ text (user_inv.cpp)
+    "g9u": dict(keys=15, distinct=1_040_187_392, generated=1_392_508_928, depth=20, user="LatestIsLast"),
+    # the same with every invariant of tests/golden/user_inv.json's U_all_hold
+    "g9uall": dict(keys=15, distinct=1_040_187_392, generated=1_392_508_928, depth=20,
+                   user=("PhaseKnown", "LatestIsLast", "LedgerSorted", "KeysKnown", "MessageRec", "HeadFirst")),
+}
+# user invariants the g9u* configs add to compaction.tla (definitions by name;
+# KeySet, ValueSet and NullKey are the module's own, restated for the library)
+USER_DEFS = {
+    "NullKey": "0",
+    "KeySet": "KeySpace \\cup {NullKey}",
+    "ValueSet": "ValueSpace \\cup {0}",
+    "PhaseKnown": "compactorState \\in {Compactor_In_PhaseOne, Compactor_In_PhaseTwoWrite,\n"
+                  "                   Compactor_In_PhaseTwoUpdateContext, Compactor_In_PhaseTwoUpdateHorizon,\n"
+                  "                   Compactor_In_PhaseTwoPersistCusror, Compactor_In_PhaseTwoDeleteLedger}",
+    "LatestIsLast": "phaseOneResult # Nil =>\n"
+                    "  \\A k \\in DOMAIN phaseOneResult.latestForKey :\n"
+                    "    /\\ messages[phaseOneResult.latestForKey[k]].key = k\n"
+                    "    /\\ \\A i \\in 1..phaseOneResult.readPosition :\n"
+                    "         messages[i].key = k => i <= phaseOneResult.latestForKey[k]",
+    "LedgerSorted": "\\A l \\in 1..CompactionTimesLimit :\n"
+                    "  compactedLedgers[l] # Nil =>\n"
+                    "    \\A a \\in 1..Len(compactedLedgers[l]) : \\A b \\in 1..Len(compactedLedgers[l]) :\n"
+                    "      a < b => compactedLedgers[l][a].id < compactedLedgers[l][b].id",
+    "KeysKnown": "\\A i \\in 1..Len(messages) : messages[i].key \\in KeySet /\\ messages[i].value \\in ValueSet",
+    "MessageRec": "\\A i \\in 1..Len(messages) :\n"
+                  "   messages[i] = [id |-> i, key |-> messages[i].key, value |-> messages[i].value]",
+    "HeadFirst": "Len(messages) > 0 => Head(messages).id = 1",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic bytes per distinct state of the fused expand kernel:
@@ -111,13 +141,22 @@ def load_microbench(rel):
     return best
 
 
+def user_invariants(cfg):
+    u = CONFIGS[cfg].get("user", ())
+    return (u,) if isinstance(u, str) else tuple(u)
+
+
 def model_for(cfg):
     import tlcgpu
     k = CONFIGS[cfg]["keys"]
+    extra = {}
+    if user_invariants(cfg):
+        extra = dict(invariants=("TypeSafe",) + user_invariants(cfg) + ("CompactionHorizonCorrectness",),
+                     user_defs=dict(USER_DEFS))
     return tlcgpu.Model(key_space=range(1, k + 1), value_space=range(1, k + 1),
                         compaction_times_limit=CONFIGS[cfg].get("C", 3),
                         model_producer=CONFIGS[cfg].get("producer", False),
-                        retain_null_key=CONFIGS[cfg].get("retain", True))
+                        retain_null_key=CONFIGS[cfg].get("retain", True), **extra)
 
 
 def algorithmic_bytes(distinct, generated, n_init, selfloops, words=1):
@@ -484,12 +523,18 @@ def main():
             "roofline": main_s["roofline"],
             "engines": {},
         }
+        if user_invariants(args.config):
+            line["config"]["invariants"] = list(model.invariants)
+            line["config"]["user_invariants"] = {n: USER_DEFS[n] for n in user_invariants(args.config)}
         if global_run:
             line["engines"]["global_hbm_fpset"] = summary(global_run)
         if exchange_run:
             line["engines"]["global_open_partition_alltoall"] = summary(exchange_run)
+            line["exchange_leg_ok"] = True
         elif exchange_error:
             line["engines"]["global_open_partition_alltoall"] = {"error": exchange_error}
+            line["exchange_leg_ok"] = False
+            line["exchange_leg_error"] = exchange_error
         return line
 
     exchange_run = exchange_error = None
@@ -502,6 +547,8 @@ def main():
         limit = float(os.environ.get("TLCG_BENCH_EXCHANGE_TIMEOUT_S", "240"))
 
         def bail():
+            # the headline line still stands; the hung leg is named at its top
+            # level (exchange_leg_ok false), never reported as a success
             if rank == 0:
                 print(json.dumps(build_line(None, f"the exchange leg did not finish within {limit:.0f} s")), flush=True)
             os._exit(0)

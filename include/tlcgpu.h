@@ -100,8 +100,11 @@ typedef struct tlcg_model {
    * definition.  A user invariant is a state predicate over the spec's
    * variables and constants (the subset user_inv.cpp documents); one outside
    * it is refused at tlcg_create / tlcg_check_model, never checked
-   * approximately.  Models with user invariants run on the global engine,
-   * one rank.  The text is copied by tlcg_create.  (ModelChecker's
+   * approximately.  Every engine and any number of ranks check them: the
+   * on-chip engines (component, component tree) as device code generated
+   * from the compiled program into their run-time specialized kernels, the
+   * global engine in a check kernel over each new level (TLCG_JIT=0 leaves
+   * such models to the global engine).  The text is copied by tlcg_create.  (ModelChecker's
    * invariant list, compaction.cfg:25-31, with invariants the user defined
    * in the .tla, compaction.tla:236-294 being the spec's own.) */
   const char* user_defs;
@@ -331,7 +334,11 @@ int tlcg_owner(tlcg_ctx* c, uint64_t state);
 /* ---- partitioned (multi-rank) level, world > 1 ----
  * tlcg_init, then per level: tlcg_expand -> exchange outboxes (e.g. RCCL
  * all-to-all) -> tlcg_inbox + copy -> tlcg_absorb -> tlcg_end_level.
- * Records are 16 bytes: {uint64 state, uint64 parent_ref}. */
+ * Records are 16 bytes: {uint64 state, uint64 parent_ref}.  A rank that is
+ * no longer running (stats.status != TLCG_RUNNING -- e.g. an on-chip engine,
+ * which completes the rank's share inside tlcg_init) returns 0 and its stats
+ * from every call of the loop, with no records; a driver loops on the
+ * combined termination as usual. */
 int tlcg_expand(tlcg_ctx* c, tlcg_stats* st);
 int tlcg_outbox(tlcg_ctx* c, int32_t dst, void** dev_records, uint64_t* n_records);
 int tlcg_inbox(tlcg_ctx* c, uint64_t n_records, void** dev_records);
@@ -378,6 +385,20 @@ int tlcg_run_node(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_stats
 int tlcg_run_node_trace(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_stats* st, uint64_t* levels,
                         int32_t cap, int32_t* n_levels, uint64_t* states, int32_t* actions, int32_t trace_cap,
                         int32_t* trace_len, char* err, int32_t err_cap);
+/* The same with the node's ranks kept across checks: tlcg_node_create builds
+ * the n contexts and their transport once, tlcg_node_run runs one whole check
+ * (the arguments and results of tlcg_run_node_trace) and may be called again;
+ * tlcg_node_destroy frees them.  A check then costs its level loop only (a
+ * context's FPSet shard and store are sized by the first check and reused,
+ * as a TLC server's FPSet outlives one exploration).  One thread of the
+ * caller at a time per node. */
+typedef struct tlcg_node tlcg_node;
+int tlcg_node_create(const tlcg_model* m, const tlcg_opts* o, int32_t n, tlcg_node** out, char* err,
+                     int32_t err_cap);
+int tlcg_node_run(tlcg_node* node, tlcg_stats* st, uint64_t* levels, int32_t cap, int32_t* n_levels,
+                  uint64_t* states, int32_t* actions, int32_t trace_cap, int32_t* trace_len, char* err,
+                  int32_t err_cap);
+void tlcg_node_destroy(tlcg_node* node);
 
 /* ---- one process per GPU over RCCL (xGMI) ----
  * Rank 0 calls tlcg_comm_unique_id and hands the 128 bytes to every rank (the

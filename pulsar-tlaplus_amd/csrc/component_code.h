@@ -72,10 +72,12 @@ struct CodeConsts {
   int hz_live;    // CompactionHorizonCorrectness at horizon = len: some position is not skipped
   int hz_false;   // ... and one of them has no witness in CompactMessages(messages, len)
   int dn0, dn1;   // DuplicateNullKeyMessage is FALSE at horizon 0 / len (ledger present)
+  u64 msgs;       // the `messages` bits of the word (UVCode)
 };
 
 TLCG_HD CodeConsts code_consts(const Layout& L, const CompMsgs& c) {
   CodeConsts k;
+  k.msgs = c.msgs;
   k.len = (uint32_t)c.len;
   const u64 cm = (c.len >= 1 && c.len <= L.N) ? (c.cm >> ((c.len - 1) * L.N)) & nmask(L.N) : 0;
   k.ledbits = (lkey)(1u | (cm << 1));
@@ -157,6 +159,39 @@ TLCG_HD W code_word(const Layout& L, const CodeConsts& K, W msgs, ckey c) {
   }
   return fset<W>(s, L.cr_sh, L.cr_w, cget(c, cc_cr(L), L.cr_w));
 }
+
+// The field view of a code for the user invariants (model.h UVWord): each
+// field from the code's bits and the component's constants, as model.h's
+// accessors would read it from code_word(msgs, c); a position or ledger index
+// outside 1..N / 1..C (which the compiled programs guard against) reads the
+// built word itself, so the view agrees with UVWord on every argument.
+template <typename W>
+struct UVCode {
+  const Layout& L;
+  const CodeConsts& K;
+  ckey c;
+  TLCG_HDM W word() const { return code_word<W>(L, K, (W)K.msgs, c); }
+  TLCG_HDM int len() const { return (int)K.len; }
+  TLCG_HDM int key(int i) const {
+    return i >= 1 && i <= L.N ? (int)fget(K.msgs, L.msg_sh + (i - 1) * L.mw, L.kb) : st_key<W>(L, word(), i);
+  }
+  TLCG_HDM int val(int i) const {
+    return i >= 1 && i <= L.N ? (int)fget(K.msgs, L.msg_sh + (i - 1) * L.mw + L.kb, L.vb) : st_val<W>(L, word(), i);
+  }
+  TLCG_HDM int phase() const { return (int)cget(c, cc_ph(L), 3); }
+  TLCG_HDM int p1r() const { return ((c >> cc_r(L)) & 1) ? (int)K.len : 0; }
+  TLCG_HDM int hz() const { return ((c >> cc_h(L)) & 1) ? (int)K.len : 0; }
+  TLCG_HDM int ctx() const { return (int)cget(c, cc_x(L), L.ctx_w); }
+  TLCG_HDM int crash() const { return (int)cget(c, cc_cr(L), L.cr_w); }
+  TLCG_HDM int curp() const { return (int)((c >> cc_cp(L)) & 1); }
+  TLCG_HDM int curh() const { return ((c >> cc_cp(L)) & 1) && ((c >> cc_ch(L)) & 1) ? (int)K.len : 0; }
+  TLCG_HDM int curc() const { return ((c >> cc_cp(L)) & 1) ? (int)cget(c, cc_cc(L), L.curc_w) : 0; }
+  TLCG_HDM int ledp(int j) const { return j >= 1 && j <= L.C ? (int)((c >> (j - 1)) & 1) : led_present<W>(L, word(), j); }
+  TLCG_HDM u64 ledm(int j) const {
+    if (j < 1 || j > L.C) return led_mask<W>(L, word(), j);
+    return ((c >> (j - 1)) & 1) ? (u64)(K.ledbits >> 1) : 0ull;
+  }
+};
 
 TLCG_HD int c_phase(const Layout& L, ckey c) { return (int)cget(c, cc_ph(L), 3); }
 // MaxCompactedLedgerId, compaction.tla:103-106
@@ -301,6 +336,7 @@ TLCG_HD int inv_dupnull_c(const Layout& L, const CodeConsts& K, ckey c) {
 }
 
 // first failing invariant in cfg order: -1 all hold, else (index << 1) | is_error
+template <typename W = u64>
 TLCG_HD int check_invariants_c(const Layout& L, const CodeConsts& K, ckey c) {
   for (int q = 0; q < L.n_inv; ++q) {
     int r;
@@ -309,7 +345,11 @@ TLCG_HD int check_invariants_c(const Layout& L, const CodeConsts& K, ckey c) {
       case INV_LEAK: r = inv_leak_c(L, c); break;
       case INV_HORIZON: r = inv_horizon_c(L, K, c); break;
       case INV_DUPNULL: r = inv_dupnull_c(L, K, c); break;
-      default: r = EV_ERROR;
+      default:
+        r = EV_ERROR;
+#ifdef TLCG_USER_INV
+        if (L.inv[q] >= INV_USER) r = tlcg_user_eval(L.inv[q] - INV_USER, UVCode<W>{L, K, c});
+#endif
     }
     if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
   }
@@ -318,6 +358,7 @@ TLCG_HD int check_invariants_c(const Layout& L, const CodeConsts& K, ckey c) {
 
 // the same without branches (the kernel's form): every invariant's outcome
 // formed, then the first failing one in cfg order selected
+template <typename W = u64>
 TLCG_HD int check_invariants_cb(const Layout& L, const CodeConsts& K, ckey c) {
   const uint32_t hb = (c >> cc_h(L)) & 1;
   const uint32_t X = cget(c, cc_x(L), L.ctx_w);
@@ -331,6 +372,9 @@ TLCG_HD int check_invariants_cb(const Layout& L, const CodeConsts& K, ckey c) {
     if (L.inv[q] == INV_LEAK) r = inv_leak_c(L, c);
     if (L.inv[q] == INV_HORIZON) r = horizon;
     if (L.inv[q] == INV_DUPNULL) r = dupnull;
+#ifdef TLCG_USER_INV
+    if (L.inv[q] >= INV_USER) r = tlcg_user_eval(L.inv[q] - INV_USER, UVCode<W>{L, K, c});
+#endif
     if (r != EV_TRUE) res = (q << 1) | (r == EV_ERROR ? 1 : 0);
   }
   return res;

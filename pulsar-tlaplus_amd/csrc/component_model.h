@@ -40,6 +40,7 @@ struct CompMsgs {
   u64 hwit;           // N <= 4: for each ledger position mask m, the positions it witnesses: N bits at m * N
   int len;            // Len(messages)
   int msgs_ok;        // TypeSafe's messages conjunct (and Len(messages) <= N)
+  u64 msgs;           // the `messages` bits of the word (user invariants: model.h UVWord)
 };
 
 TLCG_HD u64 nmask(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
@@ -47,6 +48,7 @@ TLCG_HD uint32_t lmask(int w) { return w >= 32 ? ~0u : ((1u << w) - 1); }
 
 TLCG_HD CompMsgs comp_msgs_init(const Layout& L, u64 s) {
   CompMsgs c;
+  c.msgs = s & L.msgs_mask;
   c.len = st_len(L, s);
   c.cm = c.need = 0;
   c.skip = c.null_pos = 0;
@@ -303,7 +305,12 @@ TLCG_HD int check_invariants_k(const Layout& L, const CompMsgs& c, lkey k) {
       case INV_LEAK: r = inv_leak_k(L, k); break;
       case INV_HORIZON: r = inv_horizon_k(L, c, k); break;
       case INV_DUPNULL: r = inv_dupnull_k(L, c, k); break;
-      default: r = EV_ERROR;
+      default:
+        r = EV_ERROR;
+#ifdef TLCG_USER_INV  // a user invariant on the word msgs | k << (messages' bits)
+        if (L.inv[q] >= INV_USER)
+          r = tlcg_user_eval(L.inv[q] - INV_USER, UVWord<u64>{L, c.msgs | ((u64)k << (L.msg_sh + L.N * L.mw))});
+#endif
     }
     if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
   }

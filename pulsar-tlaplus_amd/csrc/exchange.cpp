@@ -436,7 +436,7 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
   std::memset(&s, 0, sizeof s);
   // TLCG_RANK_TRACE=1: per-phase wall time of this rank's loop on stderr
   const bool trace = std::getenv("TLCG_RANK_TRACE") != nullptr;
-  double ph[7] = {0, 0, 0, 0, 0, 0, 0};  // flags, expand, counts, inbox, records, absorb, end_level
+  double ph[7] = {0, 0, 0, 0, 0, 0, 0};  // (unused), expand, counts, inbox, records, absorb, end_level
   auto clk = [] { return std::chrono::steady_clock::now(); };
   auto tick = [&](int i, std::chrono::steady_clock::time_point& t) {
     const auto n2 = clk();
@@ -463,34 +463,46 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
     std::vector<uint64_t> row(w), rows(w * (size_t)n), send((size_t)n), recv((size_t)n);
     for (; !all_tree;) {
       auto tp = clk();
-      // termination (every rank's newest level empty, or an error anywhere),
-      // and every local failure since the last collective
-      uint64_t f[3] = {failed ? 0 : s.frontier, !failed && s.status >= TLCG_VIOLATION ? 1u : 0u, failed ? 1u : 0u};
-      if (!t.allreduce(f, 3, RED_SUM, err)) return -20;
-      tick(0, tp);
-      if (f[2] || f[1] || !f[0]) break;
-      ++nlev;
-      if (tlcg_expand(c, &s) != 0) fail_local("tlcg_expand");
+      // expand this rank's newest level (an empty one too: every rank takes
+      // part in every level), then ONE collective: the counts all-gather,
+      // whose rows also carry each rank's expanded level size, error flag and
+      // failure flag.  When the rows say the search is over (every level
+      // empty, an error, a failure), the expand is undone -- its level is
+      // never absorbed -- so the counts are those of the level loop that
+      // decided first (round 3 ran a separate all-reduce before each expand).
+      const uint64_t level = failed ? 0 : s.frontier;
+      const bool erred = !failed && s.status >= TLCG_VIOLATION;
+      const bool live = !failed && s.status == TLCG_RUNNING;
+      if (live && tlcg_expand(c, &s) != 0) fail_local("tlcg_expand");
       tick(1, tp);
       for (int d = 0; d < n; ++d) {
         uint64_t k = 0;
-        if (!failed && d != me) tlcg_outbox(c, d, nullptr, &k);
+        if (live && !failed && d != me) tlcg_outbox(c, d, nullptr, &k);
         row[(size_t)d] = send[(size_t)d] = k;
       }
       row[(size_t)n] = failed ? 1 : 0;
       row[(size_t)n + 1] = ctx_inbox_cap(c);
+      row[(size_t)n + 2] = level;
+      row[(size_t)n + 3] = erred ? 1 : 0;
       if (!t.allgather_rows(row.data(), rows.data(), err)) return -20;
       tick(2, tp);
-      bool any = false, grow = false;
+      bool any = false, grow = false, stop = false;
+      uint64_t levels_total = 0;
       for (int q = 0; q < n; ++q) {
         any |= rows[(size_t)q * w + (size_t)n] != 0;
+        stop |= rows[(size_t)q * w + (size_t)n + 3] != 0;
+        levels_total += rows[(size_t)q * w + (size_t)n + 2];
         recv[(size_t)q] = q == me ? 0 : rows[(size_t)q * w + (size_t)me];
         uint64_t into_q = 0;  // what rank q receives, against its inbox
         for (int p = 0; p < n; ++p)
           if (p != q) into_q += rows[(size_t)p * w + (size_t)q];
         grow |= into_q > rows[(size_t)q * w + (size_t)n + 1];
       }
-      if (any) break;
+      if (any || stop || !levels_total) {
+        if (live && !failed) ctx_undo_expand(c, &s);
+        break;
+      }
+      ++nlev;
       uint64_t total = 0;
       for (uint64_t x : recv) total += x;
       if (grow) {

@@ -5,9 +5,10 @@
 // 8(e); TLC's distributed FPSetManager).  run_ranks() is the whole check of
 // one rank: a closed partition (no action writes `messages`) runs alone and
 // only the results are combined; an open one runs, per BFS level,
-//   tlcg_expand -> counts (all-gather) -> records (grouped send/recv of the
-//   16-B {state, parent_ref} outboxes) -> tlcg_absorb -> tlcg_end_level,
-// with a small all-reduce deciding termination.  Two transports carry it:
+//   tlcg_expand -> counts (all-gather, which also carries every rank's
+//   termination and error flags: one collective per level) -> records
+//   (grouped send/recv of the 16-B {state, parent_ref} outboxes) ->
+//   tlcg_absorb -> tlcg_end_level.  Two transports carry it:
 //   RcclTransport  -- RCCL over xGMI (one communicator per rank, on the
 //                     context's stream; one process per GPU or one thread
 //                     per GPU);
@@ -25,8 +26,9 @@ namespace tlcg {
 enum RedOp { RED_SUM = 0, RED_MIN = 1, RED_MAX = 2 };
 
 // words of a rank's row in the per-level all-gather: its record count per
-// destination, its failure flag, its inbox capacity (run_ranks)
-inline size_t row_width(int world) { return (size_t)world + 2; }
+// destination, its failure flag, its inbox capacity, the size of the level it
+// expanded, its error flag (run_ranks)
+inline size_t row_width(int world) { return (size_t)world + 4; }
 
 class Transport {
  public:
@@ -34,8 +36,9 @@ class Transport {
   virtual int rank() const = 0;
   virtual int world() const = 0;
   // row[d] = records this rank holds for rank d (row[rank] = 0), row[world] =
-  // this rank's failure flag, row[world + 1] its inbox capacity; out gets
-  // every rank's row (world x row_width(world))
+  // this rank's failure flag, row[world + 1] its inbox capacity, row[world +
+  // 2] the level it expanded, row[world + 3] its error flag; out gets every
+  // rank's row (world x row_width(world))
   virtual bool allgather_rows(const uint64_t* row, uint64_t* out, std::string* err) = 0;
   // every outbox of ctx to its owner; the inbox (already sized for the sum of
   // recv) receives them source-rank-major.  Ordered before later work on the
@@ -69,6 +72,9 @@ void ctx_disable_tree(tlcg_ctx* c);        // the next tlcg_init runs the global
 void ctx_rank_world(const tlcg_ctx* c, int* rank, int* world);
 void*& ctx_comm(tlcg_ctx* c);
 void ctx_set_error(tlcg_ctx* c, const std::string& e);
+// forget the last tlcg_expand (its level is never absorbed: the loop ends):
+// the generated counts and the pending states as before it; fresh stats
+void ctx_undo_expand(tlcg_ctx* c, tlcg_stats* st);
 
 // The local transport of n ranks driven by n threads of this process.
 struct LocalBoard;

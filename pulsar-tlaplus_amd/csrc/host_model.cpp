@@ -448,6 +448,63 @@ template int host_successors<u128>(const Layout&, u128, u128*, int*, int);
 
 using namespace tlcg;
 
+namespace {
+
+// the user invariants' views of one reachable state: a component code's
+// (component_code.h UVCode, the on-chip engines' form) against the word's
+// (model.h UVWord): every field the programs read, and each user invariant
+template <typename W>
+bool user_views_agree(const HostModel& hm, const CodeConsts& kc, W w) {
+  const Layout& L = hm.L;
+  const ckey cd = code_encode_w<W>(L, w);
+  const UVWord<W> a{L, w};
+  const UVCode<W> b{L, kc, cd};
+  if (b.word() != w) return false;
+  bool ok = a.len() == b.len() && a.phase() == b.phase() && a.p1r() == b.p1r() && a.hz() == b.hz() &&
+            a.ctx() == b.ctx() && a.crash() == b.crash() && a.curp() == b.curp() && a.curh() == b.curh() &&
+            a.curc() == b.curc();
+  for (int i = 1; i <= L.N; ++i) ok = ok && a.key(i) == b.key(i) && a.val(i) == b.val(i);
+  for (int j = 1; j <= L.C; ++j) ok = ok && a.ledp(j) == b.ledp(j) && a.ledm(j) == b.ledm(j);
+  for (int k = 0; k < hm.user->n_user && ok; ++k) ok = eval_user_v(*hm.user, k, a) == eval_user_v(*hm.user, k, b);
+  return ok;
+}
+
+// user invariants: the views on every reachable state of components
+// [first, first + n) (no Producer).  Returns the states checked, or
+// -(1 + checked) at the first disagreement.
+int64_t user_view_selfcheck(const HostModel& hm, u64 first, u64 n) {
+  const Layout& L = hm.L;
+  int64_t checked = 0;
+  if (L.N > 8 || code_bits(L) > 31) return 0;  // no on-chip engine takes the model
+  const bool wide = state_words(L) == 2;
+  for (u64 idx = first; idx < first + n && idx < hm.n_init; ++idx) {
+    const u128 s0 = wide ? init_state<u128>(L, idx) : (u128)init_state<u64>(L, idx);
+    const CodeConsts kc = code_consts(L, comp_msgs_init(L, (u64)s0));
+    std::vector<u128> todo{s0};
+    std::unordered_set<u64> seen{mix64((u64)s0) ^ (u64)(s0 >> 64)};
+    while (!todo.empty()) {
+      const u128 w = todo.back();
+      todo.pop_back();
+      if (!(wide ? user_views_agree<u128>(hm, kc, w) : user_views_agree<u64>(hm, kc, (u64)w))) return -(1 + checked);
+      ++checked;
+      u128 succ[64];
+      int ns;
+      if (wide) {
+        ns = host_successors<u128>(L, w, succ, nullptr, 64);
+      } else {
+        u64 s1[64];
+        ns = host_successors<u64>(L, (u64)w, s1, nullptr, 64);
+        for (int i = 0; i < ns && i < 64; ++i) succ[i] = s1[i];
+      }
+      for (int i = 0; i < ns && i < 64; ++i)
+        if (seen.insert(mix64((u64)succ[i]) ^ (u64)(succ[i] >> 64)).second) todo.push_back(succ[i]);
+    }
+  }
+  return checked;
+}
+
+}  // namespace
+
 extern "C" {
 
 int tlcg_abi_version(void) { return TLCG_ABI_VERSION; }
@@ -634,7 +691,7 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
   HostModel hm;
   std::string e;
   if (!m || !build_model(*m, &hm, &e) || hm.L.producer) return -1;
-  if (hm.user) return 0;  // user invariants run on the global engine only
+  if (hm.user) return user_view_selfcheck(hm, first, n);
   const Layout& L = hm.L;
   int64_t checked = 0;
   const int mb = L.led_sh;

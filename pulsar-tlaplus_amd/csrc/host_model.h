@@ -27,6 +27,9 @@ struct HostModel {
 bool compile_user_invariants(const tlcg_model& m, const HostModel& hm, const std::vector<std::string>& names,
                              UserProg* P, std::string* err);
 std::vector<std::string> user_def_names(const char* text);
+// The compiled user invariants as device code for the run-time specialized
+// kernels (user_inv.cpp; model.h tlcg_user_eval), one function per invariant.
+std::string user_device_source(const UserProg& P);
 
 // The FPSet slot-hash multiplier (multiply-shift over a T-slot table, linear
 // probing) with the fewest probe-loop trips on the insert sequence of the

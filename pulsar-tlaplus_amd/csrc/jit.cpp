@@ -34,9 +34,11 @@ std::string layout_literal(const Layout& L) {
   return o.str();
 }
 
-std::string program_source(const Layout& L) {
+std::string program_source(const Layout& L, const std::string& user) {
   std::string s = "typedef unsigned char uint8_t; typedef unsigned short uint16_t; typedef unsigned int uint32_t; typedef int int32_t;\n"
                   "typedef unsigned long uint64_t; typedef long int64_t;\n";
+  // user invariants: the headers' check functions call tlcg_user_eval (model.h)
+  if (!user.empty()) s += "#define TLCG_USER_INV 1\n";
   // tuning experiments: TLCG_JIT_DEFINES="A=1;B" becomes #define lines (part of the cache key)
   if (const char* d = std::getenv("TLCG_JIT_DEFINES")) {
     std::string all(d);
@@ -52,6 +54,7 @@ std::string program_source(const Layout& L) {
   }
   s += kJitSource;
   s += "\n" + layout_literal(L);
+  s += user;
   for (int K : {32, 64, 128, 255})
     for (const char* od : {"false", "true"})
       for (const char* code : {"false", "true"}) {
@@ -98,8 +101,9 @@ bool read_all(const std::string& p, std::vector<char>* out) {
 
 }  // namespace
 
-bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err) {
-  const std::string src = program_source(L);
+bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
+                 const std::string& user) {
+  const std::string src = program_source(L, user);
   if (const char* dump = std::getenv("TLCG_JIT_DUMP")) {  // diagnostics: the generated source
     std::ofstream f(dump);
     f << src;
@@ -139,7 +143,7 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
   return true;
 }
 
-bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
     *err = "hipGetDeviceProperties failed";
@@ -147,7 +151,7 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
   }
   std::string arch = prop.gcnArchName;
   arch = arch.substr(0, arch.find(':'));
-  const std::string src = program_source(L);
+  const std::string src = program_source(L, user);
   char key[64];
   const char* jo = std::getenv("TLCG_JIT_OPTS");
   std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2" + (jo ? jo : "")));
@@ -157,7 +161,7 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err) {
   out->cached = read_all(path, &code);
   if (!out->cached) {
     auto t0 = std::chrono::steady_clock::now();
-    if (!jit_compile(L, arch, &code, err)) return false;
+    if (!jit_compile(L, arch, &code, err, user)) return false;
     out->compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     mkdir(dir.c_str(), 0777);
     const std::string tmp = path + ".tmp" + std::to_string((long)getpid());

@@ -25,10 +25,13 @@ struct JitKernels {
 };
 
 // builds (or loads from $TLCG_JIT_CACHE, default /tmp/tlcgpu-jit) the
-// kernels specialized for L on `device`; false with a message on failure
-bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err);
+// kernels specialized for L on `device`; false with a message on failure.
+// `user`: the model's user invariants as device code (user_device_source),
+// which the kernels then evaluate in the cfg's order with the spec's own.
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user = "");
 // compile only (no device needed): the code object for `arch`
-bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err);
+bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
+                 const std::string& user = "");
 void jit_release(JitKernels* k);
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream);
 // the specialized tree kernel for cap 384 / 640 (4 groups) or 1024 / 2048 (1 group); false when not built or on a

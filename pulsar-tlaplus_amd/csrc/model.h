@@ -40,13 +40,16 @@
 #if defined(__HIPCC_RTC__)
 // compiled at run time by hipRTC (jit.cpp): the runtime headers are built in
 #define TLCG_HD __host__ __device__ __forceinline__
+#define TLCG_HDM __host__ __device__ __forceinline__
 #else
 #include <stdint.h>
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define TLCG_HD __host__ __device__ __forceinline__
+#define TLCG_HDM __host__ __device__ __forceinline__
 #else
 #define TLCG_HD static inline
+#define TLCG_HDM inline
 #endif
 #endif
 
@@ -66,6 +69,22 @@ enum Action {
 enum Invariant { INV_TYPESAFE = 0, INV_LEAK = 1, INV_HORIZON = 2, INV_DUPNULL = 3, N_INVARIANT_KINDS };
 // three-valued evaluation, as TLC: holds / false / evaluation error
 enum Eval { EV_TRUE = 0, EV_FALSE = 1, EV_ERROR = 2 };
+// Layout.inv[q] >= INV_USER: the (inv - INV_USER)-th user invariant (user_inv.h)
+constexpr int INV_USER = 16;
+#ifdef TLCG_USER_INV
+// User invariants in the run-time specialized kernels (jit.cpp): user_inv.cpp
+// (user_device_source) lowers the compiled program to straight device code,
+// defined after these headers; V is a field view of the state (UVWord below,
+// UVCode in component_code.h).  Returns EV_TRUE / EV_FALSE / EV_ERROR.
+template <class V>
+TLCG_HD int tlcg_user_eval(int k, const V& v);
+#endif
+
+// TLC's integers are 32-bit: a user invariant's +, -, * or unary - whose
+// result leaves -2^31..2^31-1 is an evaluation error ([TLC-ext] the
+// Naturals/Integers overflow check, EC.TLC_MODULE_OVERFLOW), not a wrapped
+// or 64-bit value (user_inv.h, and the generated device code)
+TLCG_HD bool ui_overflows(long long x) { return x < -2147483648LL || x > 2147483647LL; }
 
 struct Layout {
   int32_t N, C, K, ctl;        // MessageSentLimit, CompactionTimesLimit, MaxCrashTimes, ConsumeTimesLimit
@@ -156,6 +175,31 @@ template <typename W> TLCG_HD int cur_present(const Layout& L, W s) { return (in
 template <typename W> TLCG_HD int cur_h(const Layout& L, W s) { return (int)fget(s, L.cur_sh + 1, L.curh_w); }
 template <typename W> TLCG_HD int cur_c(const Layout& L, W s) { return (int)fget(s, L.cur_sh + 1 + L.curh_w, L.curc_w); }
 
+// A field view of a state for the user invariants (user_inv.h: the
+// interpreter, and the generated device code): every field a program reads,
+// as the accessors above read it from the packed word.  The component
+// engines' views (component_code.h UVCode) return the same values from their
+// encodings; tlcg_host_user_view_selfcheck compares them on every reachable
+// state of whole components.
+template <typename W>
+struct UVWord {
+  const Layout& L;
+  W s;
+  TLCG_HDM int len() const { return st_len(L, s); }
+  TLCG_HDM int key(int i) const { return st_key(L, s, i); }  // key index of messages[i]
+  TLCG_HDM int val(int i) const { return st_val(L, s, i); }  // value index
+  TLCG_HDM int phase() const { return st_phase(L, s); }
+  TLCG_HDM int p1r() const { return st_p1r(L, s); }
+  TLCG_HDM int hz() const { return st_hz(L, s); }
+  TLCG_HDM int ctx() const { return st_ctx(L, s); }
+  TLCG_HDM int crash() const { return st_crash(L, s); }
+  TLCG_HDM int curp() const { return cur_present(L, s); }
+  TLCG_HDM int curh() const { return cur_h(L, s); }
+  TLCG_HDM int curc() const { return cur_c(L, s); }
+  TLCG_HDM int ledp(int j) const { return led_present(L, s, j); }
+  TLCG_HDM u64 ledm(int j) const { return led_mask(L, s, j); }
+};
+
 TLCG_HD int popcount64(u64 x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __popcll(x);
@@ -235,6 +279,16 @@ TLCG_HD W init_state(const Layout& L, u64 idx) {
     s = fset(s, L.msg_sh + (i - 1) * L.mw, L.mw, k | (v << L.kb));
   }
   return s;
+}
+
+// The inverse of init_state on an initial state: its enumeration number.
+template <typename W = u64>
+TLCG_HD u64 init_index(const Layout& L, W s) {
+  if (L.producer) return 0;
+  u64 idx = 0;
+  for (int i = L.N; i >= 1; --i)
+    idx = idx * (u64)L.nkv + (u64)st_key(L, s, i) + (u64)st_val(L, s, i) * (u64)L.nk;
+  return idx;
 }
 
 // Successor ordinal = position in TLC's successor enumeration of one state:

@@ -84,7 +84,8 @@ __global__ __launch_bounds__(BLOCK) void k_user_check(Layout L, const UserProg* 
   if (i >= n) return;
   const int c = check_invariants_all(L, *P, states[i]);
   if (c < 0) return;
-  const u64 dkey = level0 ? i : (parents[i] & ((1ull << 56) - 1));
+  // (level 0: the Init number, which is the store position on one rank only)
+  const u64 dkey = level0 ? init_index(L, states[i]) : (parents[i] & ((1ull << 56) - 1));
   atomicMin(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
 }
 
@@ -779,6 +780,7 @@ struct tlcg_ctx {
   tlcg_opts opts;
   HostModel hm;
   std::string user_defs;                 // model.user_defs points here (tlcg_create copies the caller's text)
+  std::string user_src;                  // the user invariants as device code (user_device_source), for jit_build
   uint32_t comp_mult = 0, tree_mult = 0;  // tuned slot-hash multipliers (0: not yet)
   uint32_t tree_disp_mult = 0;               // the tree's closed-mode slot displacements (build_slot_disp)
   uint16_t tree_disp[TREE_DISP] = {};
@@ -1831,13 +1833,20 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
 // device counters of a component pass (d_comp / h_comp)
 constexpr int kCompCounters = 2 * COMP_MAXLV + 7;
 
+// user invariants run only in the specialized kernels (jit.cpp: their device
+// code is generated per model), so TLCG_JIT=0 leaves them to the global engine
+bool jit_off() {
+  const char* jv = std::getenv("TLCG_JIT");
+  return jv && std::atoi(jv) == 0;
+}
+
 // applicable: `messages` immutable, one rank's components all local, local key fits 32 bits,
-// N <= 8 (component_model.h packs N x N bit masks)
+// N <= 8 (component_model.h packs N x N bit masks); user invariants need the specialized kernels
 bool component_applicable(const tlcg_ctx* c) {
   const Layout& L = c->hm.L;
   const int mb = L.msg_sh + L.N * L.mw;
   return !L.producer && !c->opts.tlc_order && c->closed && L.bits <= 63 && L.bits - mb <= 32 && L.N <= 8 &&
-         c->hm.n_init < (1ull << 36) && !c->hm.user;
+         c->hm.n_init < (1ull << 36) && !(c->hm.user && jit_off());
 }
 
 // Fold the COMP_STRIPES copies of a pass's counters into out[0, kCompCounters)
@@ -1898,13 +1907,14 @@ int run_component(tlcg_ctx* c) {
   // specialize the kernels for these constants when the run is large enough
   // to repay a hipRTC compile (env TLCG_JIT=0/1 forces)
   const char* jv = std::getenv("TLCG_JIT");
-  const bool want_jit = jv ? std::atoi(jv) != 0 : (r1 - r0) >= 65536;
+  const bool want_jit = c->hm.user || (jv ? std::atoi(jv) != 0 : (r1 - r0) >= 65536);
   if (want_jit && c->jit_state == 0) {
     std::string e;
-    c->jit_state = jit_build(L, c->opts.device, &c->jit, &e) ? 1 : -1;
+    c->jit_state = jit_build(L, c->opts.device, &c->jit, &e, c->user_src) ? 1 : -1;
     if (c->jit_state < 0) c->jit_error = e;
   }
   c->jit_used = want_jit && c->jit_state == 1;
+  if (c->hm.user && !c->jit_used) return 0;  // (user invariants: the global engine, k_user_check)
   const char* cv = std::getenv("TLCG_CODE");  // 0: 32-bit local keys throughout (A/B)
   c->comp_code = code_bits(L) <= 16 && !(cv && std::atoi(cv) == 0);
   if (c->comp_code && !c->comp_mult) {
@@ -2049,7 +2059,7 @@ bool tree_applicable(const tlcg_ctx* c) {
   const char* tv = std::getenv("TLCG_TREE");
   return L.producer && !(tv && std::atoi(tv) == 0) && !c->no_tree && !c->opts.tlc_order && c->words == 1 &&
          L.bits - mb <= 31 && L.N >= 1 && L.N <= 8 && !c->opts.outdegree && L.nkv >= 1 && c->hm.n_init >= 1 &&
-         !c->opts.device_store_cap && !c->opts.fpset_spill && !c->hm.user;
+         !c->opts.device_store_cap && !c->opts.fpset_spill && !(c->hm.user && jit_off());
 }
 
 // the closed mode (tree.h): no Producer, a closed partition, components the
@@ -2061,7 +2071,7 @@ bool tree_closed_applicable(const tlcg_ctx* c) {
   return !L.producer && !(tv && std::atoi(tv) == 0) && c->closed && !c->opts.tlc_order && !c->opts.outdegree &&
          code_bits(L) <= 31 && L.N >= 1 && L.N <= 8 && (c->words == 1 || c->words == 2) &&
          c->hm.n_init >= 1 && c->hm.n_init < (1ull << 40) && !c->opts.device_store_cap && !c->opts.fpset_spill &&
-         !c->hm.user;
+         !(c->hm.user && (jit_off() || L.msgs_mask_hi));
 }
 
 // Run the component tree.  Producer modelled: every layer, chunks of 384
@@ -2126,13 +2136,14 @@ int run_tree(tlcg_ctx* c) {
   // the layout-specialized kernels (jit.cpp) when the tree is large enough
   // to repay a hipRTC compile (env TLCG_JIT=0/1 forces)
   const char* jv = std::getenv("TLCG_JIT");
-  const bool want_jit = (jv ? std::atoi(jv) != 0 : comps >= 4096) && groups == 4;
+  const bool want_jit = (c->hm.user || (jv ? std::atoi(jv) != 0 : comps >= 4096)) && groups == 4;
   if (want_jit && c->jit_state == 0) {
     std::string e;
-    c->jit_state = jit_build(L, c->opts.device, &c->jit, &e) ? 1 : -1;
+    c->jit_state = jit_build(L, c->opts.device, &c->jit, &e, c->user_src) ? 1 : -1;
     if (c->jit_state < 0) c->jit_error = e;
   }
   c->jit_used = want_jit && c->jit_state == 1;
+  if (c->hm.user && !c->jit_used) return 0;  // (user invariants: the global engine, k_user_check)
   const int words = c->words;
   if (closed && !c->tree_mult) {  // (640-slot tables, 16 lanes per component; tree_body.h)
     const char* tv = std::getenv("TLCG_TUNE_MULT");
@@ -2563,6 +2574,15 @@ bool step_level(tlcg_ctx* c) {
 
 namespace tlcg {
 
+void ctx_undo_expand(tlcg_ctx* c, tlcg_stats* st) {
+  if (c->engine == TLCG_ENGINE_GLOBAL && !c->gen_at.empty() && c->pending == c->h_ctr->n_new) {
+    c->generated = c->gen_at.back();
+    c->gen_at.pop_back();
+    c->pending = 0;
+  }
+  fill_stats(c, st);
+}
+
 // The counterexample of a multi-rank run (the parent references
 // walked across the ranks' stores, host-mediated).  Collective: every rank of
 // t calls it with the same `first` (the rank holding the first error,
@@ -2674,16 +2694,7 @@ int tlcg_create(const tlcg_model* m, const tlcg_opts* o, tlcg_ctx** out) {
   }
   c->user_defs = m->user_defs ? m->user_defs : "";
   c->model.user_defs = m->user_defs ? c->user_defs.c_str() : nullptr;
-  if (c->hm.user && c->opts.world != 1) {
-    c->err = "user invariants are checked on one rank (world 1)";
-    *out = c;
-    return -2;
-  }
-  if (c->hm.user && (c->opts.engine == TLCG_ENGINE_COMPONENT || c->opts.engine == TLCG_ENGINE_TREE)) {
-    c->err = "user invariants are checked by the global engine";
-    *out = c;
-    return -2;
-  }
+  if (c->hm.user) c->user_src = user_device_source(*c->hm.user);
   c->words = state_words(c->hm.L);
   // partition key: `messages` alone when it is immutable (no Producer), so a
   // state's whole successor graph stays on its owner rank; else the state.
@@ -2833,7 +2844,9 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
       return 0;
     }
     if (c->opts.engine == TLCG_ENGINE_COMPONENT) {
-      c->err = "a component does not fit on chip (over 255 states or 48 levels); use the global engine";
+      c->err = c->hm.user && !c->jit_used
+                   ? "user invariants need the specialized kernels, which could not be built: " + c->jit_error
+                   : "a component does not fit on chip (over 255 states or 48 levels); use the global engine";
       return -12;
     }
   }
@@ -3457,7 +3470,7 @@ int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t 
   std::string e;
   if (!m || !build_model(*m, &hm, &e)) return -1;
   std::vector<char> code;
-  if (!jit_compile(hm.L, arch ? arch : "gfx950", &code, &e)) {
+  if (!jit_compile(hm.L, arch ? arch : "gfx950", &code, &e, hm.user ? user_device_source(*hm.user) : "")) {
     if (err && cap > 0) std::snprintf(err, (size_t)cap, "%s", e.c_str());
     return -2;
   }
@@ -3501,14 +3514,16 @@ int tlcg_owner(tlcg_ctx* c, uint64_t state) {
 int tlcg_expand(tlcg_ctx* c, tlcg_stats* st) {
   const DeviceGuard dg(c);
   if (!c || !c->inited) return -1;
+  // a finished rank returns its stats, whichever engine finished it (an
+  // on-chip engine completes this rank's share inside tlcg_init: ADVICE r3)
+  if (c->status != TLCG_RUNNING) {
+    fill_stats(c, st);
+    return 0;
+  }
   if (c->engine != TLCG_ENGINE_GLOBAL) {
     c->err = "the on-chip engine completed this rank's share in tlcg_init: there is no level to expand "
              "(tlcg_opts.engine = TLCG_ENGINE_GLOBAL for the exchange)";
     return -2;
-  }
-  if (c->status != TLCG_RUNNING) {
-    fill_stats(c, st);
-    return 0;
   }
   const HostModel& hm = c->hm;
   const int depth = (int)c->level_base.size() - 1;
@@ -3737,8 +3752,12 @@ int tlcg_end_level(tlcg_ctx* c, tlcg_stats* st) {
     if (c->opts.fpset_spill && (n_new = tier_filter_level(c, d, n_new)) == ~0ull) return -10;
     c->level_base.push_back(d + n_new);  // empty levels kept (see run_init)
     c->pending = 0;
-    if (c->h_ctr->event != NO_EVENT) {
-      if (!resolve_event(c, c->h_ctr->event, depth)) return -10;
+    // the user invariants on the level's new states, the absorbed ones included
+    const u64 uev = user_check_level(c, d, n_new, false);
+    if (uev == ~0ull - 1) return -10;
+    const u64 ev = std::min<u64>(c->h_ctr->event, uev);
+    if (ev != NO_EVENT) {
+      if (!resolve_event(c, ev, depth)) return -10;
     }
   }
   fill_stats(c, st);

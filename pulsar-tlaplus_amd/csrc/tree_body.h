@@ -229,7 +229,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         else st[pos] = code_word<W>(L, kc, msgs, key);
 #endif
 #ifndef TLCG_TREE_NO_INV  // (experiment only: what the invariants cost)
-        if (!TLCG_TREE_INV_AT_EXPAND && check_invariants_cb(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
+        if (!TLCG_TREE_INV_AT_EXPAND && check_invariants_cb<W>(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
 #endif
       } else {
         st[pos] = msgs | ((u64)key << mb);
@@ -326,7 +326,12 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     // runs in one step whose lanes j and j + S/2 both expand state j, the
     // first inserting its compactor successor and the second its BrokerCrash
     // one, so the depth takes one insert instead of two (the idle half of
-    // the group does the second); the store order is the same
+    // the group does the second); the store order is the same, except when a
+    // compactor successor and a BrokerCrash successor of the same depth are one
+    // state: then either lane's CAS may take it, so its position and
+    // recorded parent may differ from the two-insert order.  Counts, depths and
+    // the state set are unaffected, and no trace is read from the tree's
+    // parents (an error is reported by the global engine's TLC-order run)
     constexpr bool PAIR = CLOSED ? TLCG_TREE_PAIR : TLCG_TREE_PAIR_OPEN;
     const bool pairm = PAIR && have && f1 - f0 <= S / 2;
     const bool roleb = pairm && sub >= S / 2;  // (pair mode: this lane inserts the BrokerCrash successor)
@@ -352,7 +357,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       bool crash;
       if constexpr (CLOSED) {
 #ifndef TLCG_TREE_NO_INV
-        if (TLCG_TREE_INV_AT_EXPAND && ok && check_invariants_cb(L, kc, k) >= 0) flags |= TREE_EVENT;
+        if (TLCG_TREE_INV_AT_EXPAND && ok && check_invariants_cb<W>(L, kc, k) >= 0) flags |= TREE_EVENT;
 #endif
         r = ok ? compactor_step_cb(L, kc, k, &t, &act) : 0;
         crash = ok && crash_step_c(L, k, &t2);

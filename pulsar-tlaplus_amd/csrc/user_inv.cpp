@@ -2015,6 +2015,168 @@ bool compile_user_invariants(const tlcg_model& m, const HostModel& hm, const std
   return true;
 }
 
+// ---------------------------------------------------------------- device code
+// The program of every user invariant lowered to straight C++ for the
+// run-time specialized kernels (jit.cpp; model.h tlcg_user_eval): one
+// function per invariant, the registers as locals, each instruction as the
+// interpreter (user_inv.h eval_user_v) executes it, jumps as gotos, the
+// KeySet / ValueSet tables as constant expressions.  Under hipRTC the
+// layout's constants fold, so a field read is a shift and a mask of the
+// engine's own encoding (the view V: a component code, a local key, a word).
+namespace {
+
+// x -> t[x] for x in 0..63 (0 past n), as an expression in `x`: arithmetic
+// when the table is affine on 0..n-1 with t[0] = 0 (the spec's index 0 is
+// NullKey / the null value), else a select chain
+std::string table_expr(const int32_t* t, int n, const std::string& x) {
+  bool affine = n >= 1 && t[0] == 0;
+  long long step = n >= 2 ? (long long)t[1] - t[0] : 1;
+  for (int i = 0; i < n && affine; ++i) affine = (long long)t[i] == step * i;
+  std::ostringstream o;
+  if (affine) {
+    o << "((" << x << ") < " << n << " ? " << step << "LL * (" << x << ") : 0LL)";
+    return o.str();
+  }
+  o << "(";
+  for (int i = 0; i < n; ++i) o << "(" << x << ") == " << i << " ? " << t[i] << "LL : ";
+  o << "0LL)";
+  return o.str();
+}
+
+// membership of `x` in the ascending t[0..n-1]
+std::string member_expr(const int32_t* t, int n, const std::string& x) {
+  bool range = n >= 1;
+  for (int i = 1; i < n && range; ++i) range = t[i] == t[i - 1] + 1;
+  std::ostringstream o;
+  if (range) {
+    o << "((long long)((" << x << ") >= " << t[0] << "LL && (" << x << ") <= " << t[n - 1] << "LL))";
+    return o.str();
+  }
+  o << "((long long)(false";
+  for (int i = 0; i < n; ++i) o << " || (" << x << ") == " << t[i] << "LL";
+  o << "))";
+  return o.str();
+}
+
+}  // namespace
+
+std::string user_device_source(const UserProg& P) {
+  std::ostringstream o;
+  o << "namespace tlcg {\n";
+  const int n = P.n_ins;
+  std::vector<bool> target((size_t)n + 1, false);
+  for (int k = 0; k < P.n_user; ++k) target[(size_t)P.entry[k]] = true;
+  for (int i = 0; i < n; ++i) {
+    const UInsn& in = P.ins[i];
+    if (in.op == U_JMP || in.op == U_JZ || in.op == U_JNZ) target[(size_t)in.imm] = true;
+  }
+  int maxreg = 0;
+  for (int i = 0; i < n; ++i)
+    maxreg = std::max({maxreg, (int)P.ins[i].a + 1, (int)P.ins[i].b + 1, (int)P.ins[i].c + 1});
+  maxreg = std::max(maxreg, 1);
+  auto R = [](int r) { return "r" + std::to_string(r); };
+  for (int k = 0; k < P.n_user; ++k) {
+    o << "template <class V>\nTLCG_HD int tlcg_user_inv_" << k << "(const V& v) {\n";
+    o << "  long long ";
+    for (int r = 0; r < maxreg; ++r) o << R(r) << " = 0" << (r + 1 < maxreg ? ", " : ";\n");
+    o << "  int loops = 0;\n  (void)loops;\n";
+    o << "  goto L" << P.entry[k] << ";\n";
+    for (int i = 0; i < n; ++i) {
+      const UInsn& in = P.ins[i];
+      if (target[(size_t)i]) o << "L" << i << ":\n";
+      const std::string a = R(in.a), b = R(in.b), c = R(in.c);
+      auto jump = [&](const std::string& cond) {
+        const bool back = in.imm <= i;
+        o << "  if (" << cond << ") { ";
+        if (back) o << "if (++loops > " << UI_MAXLOOP << ") return EV_ERROR; ";
+        o << "goto L" << in.imm << "; }\n";
+      };
+      auto ovf = [&]() { o << "  if (ui_overflows(" << a << ")) return EV_ERROR;\n"; };
+      switch (in.op) {
+        case U_LDI: o << "  " << a << " = " << in.imm << "LL;\n"; break;
+        case U_MOV: o << "  " << a << " = " << b << ";\n"; break;
+        case U_LEN: o << "  " << a << " = v.len();\n"; break;
+        case U_MKEY:
+          o << "  { const int x = v.key((int)" << b << ") & " << (UI_MAXSET - 1) << "; " << a << " = "
+            << table_expr(P.keyval, P.nk, "x") << "; }\n";
+          break;
+        case U_MVAL:
+          o << "  { const int x = v.val((int)" << b << ") & " << (UI_MAXSET - 1) << "; " << a << " = "
+            << table_expr(P.valval, P.nv, "x") << "; }\n";
+          break;
+        case U_PHASE: o << "  " << a << " = " << UV_PHASE0 << "LL + v.phase();\n"; break;
+        case U_P1R: o << "  " << a << " = v.p1r();\n"; break;
+        case U_HZ: o << "  " << a << " = v.hz();\n"; break;
+        case U_CTX: o << "  " << a << " = v.ctx();\n"; break;
+        case U_CRASH: o << "  " << a << " = v.crash();\n"; break;
+        case U_CURP: o << "  " << a << " = v.curp();\n"; break;
+        case U_CURH: o << "  " << a << " = v.curh();\n"; break;
+        case U_CURC: o << "  " << a << " = v.curc();\n"; break;
+        case U_LEDP: o << "  " << a << " = v.ledp((int)" << b << ");\n"; break;
+        case U_LEDM: o << "  " << a << " = (long long)v.ledm((int)" << b << ");\n"; break;
+        case U_LFK:
+          o << "  { long long best = 0;\n"
+            << "    for (int i = 1; i <= (int)" << c << " && i <= v.L.N; ++i) {\n"
+            << "      const int x = v.key(i) & " << (UI_MAXSET - 1) << ";\n"
+            << "      if (" << table_expr(P.keyval, P.nk, "x") << " == " << b << ") best = i;\n"
+            << "    }\n    " << a << " = best; }\n";
+          break;
+        case U_ADD: o << "  " << a << " = " << b << " + " << c << ";\n"; ovf(); break;
+        case U_SUB: o << "  " << a << " = " << b << " - " << c << ";\n"; ovf(); break;
+        case U_MUL: o << "  " << a << " = " << b << " * " << c << ";\n"; ovf(); break;
+        case U_DIV:
+          o << "  { const long long q = " << b << " / " << c << "; " << a << " = (" << b << " % " << c
+            << " != 0 && ((" << b << " < 0) != (" << c << " < 0))) ? q - 1 : q; }\n";
+          break;
+        case U_MOD:
+          o << "  { const long long m = " << b << " % " << c << "; " << a << " = m < 0 ? m + " << c << " : m; }\n";
+          break;
+        case U_NEG: o << "  " << a << " = -" << b << ";\n"; ovf(); break;
+        case U_EQ: o << "  " << a << " = " << b << " == " << c << ";\n"; break;
+        case U_NE: o << "  " << a << " = " << b << " != " << c << ";\n"; break;
+        case U_LT: o << "  " << a << " = " << b << " < " << c << ";\n"; break;
+        case U_LE: o << "  " << a << " = " << b << " <= " << c << ";\n"; break;
+        case U_NOT: o << "  " << a << " = !" << b << ";\n"; break;
+        case U_AND: o << "  " << a << " = " << b << " & " << c << ";\n"; break;
+        case U_OR: o << "  " << a << " = " << b << " | " << c << ";\n"; break;
+        case U_ADDI: o << "  " << a << " = " << b << " + " << in.imm << "LL;\n"; break;
+        case U_BIT:
+          o << "  " << a << " = (" << c << " >= 1 && " << c << " <= 63) ? (" << b << " >> (" << c
+            << " - 1)) & 1 : 0;\n";
+          break;
+        case U_POPC: o << "  " << a << " = popcount64((u64)" << b << ");\n"; break;
+        case U_NTH:
+          o << "  { u64 m = (u64)" << b << "; long long j = " << c << ", pos = 0;\n"
+            << "    for (int p = 1; p <= 63 && m; ++p, m >>= 1)\n"
+            << "      if ((m & 1) && --j == 0) { pos = p; break; }\n"
+            << "    " << a << " = j > 0 || " << c << " < 1 ? 0 : pos; }\n";
+          break;
+        case U_MASK: o << "  " << a << " = (long long)((1ull << (" << b << " & 63)) - 1);\n"; break;
+        case U_KIN:
+          o << "  " << a << " = "
+            << (in.imm ? member_expr(P.valsorted, P.nv, b) : member_expr(P.keysorted, P.nk, b)) << ";\n";
+          break;
+        case U_KAT:
+          o << "  { const int x = (int)" << b << " & " << (UI_MAXSET - 1) << "; " << a << " = "
+            << (in.imm ? table_expr(P.valsorted, P.nv, "x") : table_expr(P.keysorted, P.nk, "x")) << "; }\n";
+          break;
+        case U_JMP: jump("true"); break;
+        case U_JZ: jump("!" + a); break;
+        case U_JNZ: jump(a); break;
+        case U_ERR: o << "  return EV_ERROR;\n"; break;
+        case U_RET: o << "  return " << a << " ? EV_TRUE : EV_FALSE;\n"; break;
+        default: o << "  return EV_ERROR;\n"; break;
+      }
+    }
+    if (target[(size_t)n]) o << "L" << n << ":\n";
+    o << "  return EV_ERROR;\n}\n";
+  }
+  o << "template <class V>\nTLCG_HD int tlcg_user_eval(int k, const V& v) {\n  switch (k) {\n";
+  for (int k = 0; k < P.n_user; ++k) o << "    case " << k << ": return tlcg_user_inv_" << k << "(v);\n";
+  o << "  }\n  return EV_ERROR;\n}\n}  // namespace tlcg\n";
+  return o.str();
+}
+
 // the names of the definitions in a user_defs text, in order
 std::vector<std::string> user_def_names(const char* text) {
   std::vector<std::string> out;

@@ -23,7 +23,7 @@ namespace tlcg {
 constexpr int UI_MAXINS = 4096;  // instructions over all user invariants of a model (32 KB, device memory)
 constexpr int UI_MAXREG = 64;    // registers (int64) of the program
 constexpr int UI_MAXSET = 64;    // KeySet / ValueSet elements (incl. NullKey / NullValue)
-constexpr int INV_USER = 16;     // tlcg_model.invariants: INV_USER + k = the k-th user invariant
+// (INV_USER, model.h: tlcg_model.invariants INV_USER + k = the k-th user invariant)
 
 // model values as integers (compactorState's phases and Nil); disjoint from
 // every integer the spec's variables take, and compared only with each other
@@ -84,39 +84,49 @@ struct UserProg {
   UInsn ins[UI_MAXINS];
 };
 
-// Runs user invariant k on state s: EV_TRUE / EV_FALSE / EV_ERROR.
-template <typename W>
-TLCG_HD int eval_user(const Layout& L, const UserProg& P, int k, W s) {
+// (+, -, * and unary - past TLC's 32-bit integers: model.h ui_overflows)
+// Programs run at most UI_MAXLOOP taken backward jumps (quantifier / CHOOSE
+// iterations; forward code runs each instruction at most once), then fail as
+// an evaluation error.  The generated device code (user_inv.cpp) counts the
+// same way, so both give the same result on every state.
+constexpr int UI_MAXLOOP = 1 << 20;
+
+// Runs user invariant k on the state behind view v (model.h UVWord, or an
+// on-chip engine's view): EV_TRUE / EV_FALSE / EV_ERROR.
+template <class V>
+TLCG_HD int eval_user_v(const UserProg& P, int k, const V& v) {
   long long r[UI_MAXREG];
   int pc = P.entry[k];
-  for (int steps = 0; steps < (1 << 20); ++steps) {  // (a program is a DAG plus bounded loops)
+  int loops = 0;
+  for (;;) {
+    const int at = pc;
     const UInsn in = P.ins[pc++];
     switch (in.op) {
       case U_LDI: r[in.a] = in.imm; break;
       case U_MOV: r[in.a] = r[in.b]; break;
-      case U_LEN: r[in.a] = st_len(L, s); break;
-      case U_MKEY: r[in.a] = P.keyval[st_key(L, s, (int)r[in.b]) & (UI_MAXSET - 1)]; break;
-      case U_MVAL: r[in.a] = P.valval[st_val(L, s, (int)r[in.b]) & (UI_MAXSET - 1)]; break;
-      case U_PHASE: r[in.a] = UV_PHASE0 + st_phase(L, s); break;
-      case U_P1R: r[in.a] = st_p1r(L, s); break;
-      case U_HZ: r[in.a] = st_hz(L, s); break;
-      case U_CTX: r[in.a] = st_ctx(L, s); break;
-      case U_CRASH: r[in.a] = st_crash(L, s); break;
-      case U_CURP: r[in.a] = cur_present(L, s); break;
-      case U_CURH: r[in.a] = cur_h(L, s); break;
-      case U_CURC: r[in.a] = cur_c(L, s); break;
-      case U_LEDP: r[in.a] = led_present(L, s, (int)r[in.b]); break;
-      case U_LEDM: r[in.a] = (long long)led_mask(L, s, (int)r[in.b]); break;
+      case U_LEN: r[in.a] = v.len(); break;
+      case U_MKEY: r[in.a] = P.keyval[v.key((int)r[in.b]) & (UI_MAXSET - 1)]; break;
+      case U_MVAL: r[in.a] = P.valval[v.val((int)r[in.b]) & (UI_MAXSET - 1)]; break;
+      case U_PHASE: r[in.a] = UV_PHASE0 + v.phase(); break;
+      case U_P1R: r[in.a] = v.p1r(); break;
+      case U_HZ: r[in.a] = v.hz(); break;
+      case U_CTX: r[in.a] = v.ctx(); break;
+      case U_CRASH: r[in.a] = v.crash(); break;
+      case U_CURP: r[in.a] = v.curp(); break;
+      case U_CURH: r[in.a] = v.curh(); break;
+      case U_CURC: r[in.a] = v.curc(); break;
+      case U_LEDP: r[in.a] = v.ledp((int)r[in.b]); break;
+      case U_LEDM: r[in.a] = (long long)v.ledm((int)r[in.b]); break;
       case U_LFK: {
         long long best = 0;
-        for (int i = 1; i <= (int)r[in.c] && i <= L.N; ++i)
-          if (P.keyval[st_key(L, s, i) & (UI_MAXSET - 1)] == r[in.b]) best = i;
+        for (int i = 1; i <= (int)r[in.c] && i <= v.L.N; ++i)
+          if (P.keyval[v.key(i) & (UI_MAXSET - 1)] == r[in.b]) best = i;
         r[in.a] = best;
         break;
       }
-      case U_ADD: r[in.a] = r[in.b] + r[in.c]; break;
-      case U_SUB: r[in.a] = r[in.b] - r[in.c]; break;
-      case U_MUL: r[in.a] = r[in.b] * r[in.c]; break;
+      case U_ADD: r[in.a] = r[in.b] + r[in.c]; if (ui_overflows(r[in.a])) return EV_ERROR; break;
+      case U_SUB: r[in.a] = r[in.b] - r[in.c]; if (ui_overflows(r[in.a])) return EV_ERROR; break;
+      case U_MUL: r[in.a] = r[in.b] * r[in.c]; if (ui_overflows(r[in.a])) return EV_ERROR; break;
       case U_DIV: {
         const long long q = r[in.b] / r[in.c];
         r[in.a] = (r[in.b] % r[in.c] != 0 && ((r[in.b] < 0) != (r[in.c] < 0))) ? q - 1 : q;
@@ -127,7 +137,7 @@ TLCG_HD int eval_user(const Layout& L, const UserProg& P, int k, W s) {
         r[in.a] = m < 0 ? m + r[in.c] : m;
         break;
       }
-      case U_NEG: r[in.a] = -r[in.b]; break;
+      case U_NEG: r[in.a] = -r[in.b]; if (ui_overflows(r[in.a])) return EV_ERROR; break;
       case U_EQ: r[in.a] = r[in.b] == r[in.c]; break;
       case U_NE: r[in.a] = r[in.b] != r[in.c]; break;
       case U_LT: r[in.a] = r[in.b] < r[in.c]; break;
@@ -170,8 +180,14 @@ TLCG_HD int eval_user(const Layout& L, const UserProg& P, int k, W s) {
       case U_RET: return r[in.a] ? EV_TRUE : EV_FALSE;
       default: return EV_ERROR;
     }
+    if (pc <= at && ++loops > UI_MAXLOOP) return EV_ERROR;  // a taken backward jump
   }
-  return EV_ERROR;
+}
+
+// Runs user invariant k on state s: EV_TRUE / EV_FALSE / EV_ERROR.
+template <typename W>
+TLCG_HD int eval_user(const Layout& L, const UserProg& P, int k, W s) {
+  return eval_user_v(P, k, UVWord<W>{L, s});
 }
 
 // Every invariant of the cfg in its order -- the spec's own (model.h) and the

@@ -622,7 +622,14 @@ bool bind_model(const Config& cfg, const Module& mod, bool deadlock_flag, tlcg_m
         defs = user_defs_text(mod, &index);
         m->user_defs = defs.c_str();
       }
-      m->invariants[m->n_invariants++] = TLCG_INV_USER + index[name];
+      // a definition without body text (the built-in module's own Init, Next,
+      // ...) is not in the index: refuse it rather than bind another one
+      const auto it = index.find(name);
+      if (it == index.end()) {
+        *err = "Error: invariant " + name + " cannot be checked: its definition text is not available.";
+        return false;  // (*exit_code is 151)
+      }
+      m->invariants[m->n_invariants++] = TLCG_INV_USER + it->second;
       continue;
     }
     m->invariants[m->n_invariants++] = id;

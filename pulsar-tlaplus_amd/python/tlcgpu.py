@@ -138,6 +138,10 @@ def load_library(path: str = LIB_PATH):
         "tlcg_run_node": (C.c_int, [M, O, I32, S, C.POINTER(U64), I32, C.POINTER(I32), C.c_char_p, I32]),
         "tlcg_run_node_trace": (C.c_int, [M, O, I32, S, C.POINTER(U64), I32, C.POINTER(I32), C.POINTER(U64),
                                           C.POINTER(I32), I32, C.POINTER(I32), C.c_char_p, I32]),
+        "tlcg_node_create": (C.c_int, [M, O, I32, C.POINTER(P), C.c_char_p, I32]),
+        "tlcg_node_run": (C.c_int, [P, S, C.POINTER(U64), I32, C.POINTER(I32), C.POINTER(U64), C.POINTER(I32), I32,
+                                    C.POINTER(I32), C.c_char_p, I32]),
+        "tlcg_node_destroy": (None, [P]),
         "tlcg_comm_available": (C.c_int, []),
         "tlcg_comm_unique_id": (C.c_int, [P, I32]),
         "tlcg_comm_init": (C.c_int, [P, P, I32]),
@@ -545,44 +549,86 @@ def run(model: Model, **kw) -> Result:
         ck.close()
 
 
-def run_node(model: Model, ranks: int, device: int = 0, log2_fpset_slots: int = 0, state_capacity: int = 0,
-             partition: int = 0, engine: str = "auto", spill: bool = False, device_store_cap: int = 0,
-             fpset_spill: bool = False, log2_fpset_max: int = 0) -> Result:
-    """The check by this one process on `ranks` contexts, rank r on device
-    r mod device_count (tlcg_run_node_trace; `tlc-hip -gpus N`).  On an error
-    .trace is the counterexample walked across the ranks' stores (a shortest
-    one; TLC -workers 1's own trace: Checker(..., tlc_order=True))."""
-    lib = load_library()
-    m = model.to_c()
+def _node_opts(device=0, log2_fpset_slots=0, state_capacity=0, partition=0, engine="auto", spill=False,
+               device_store_cap=0, fpset_spill=False, log2_fpset_max=0):
     o = tlcg_opts()
     o.device, o.log2_fpset_slots, o.state_capacity, o.partition = device, log2_fpset_slots, state_capacity, partition
     o.engine = ENGINES[engine]
     o.spill, o.device_store_cap = int(spill), device_store_cap
     o.fpset_spill, o.log2_fpset_max = int(fpset_spill), log2_fpset_max
-    st = tlcg_stats()
-    lv = (C.c_uint64 * 65536)()
-    n = C.c_int32()
-    err = C.create_string_buffer(1024)
-    w = state_words(model)
-    tcap = 4096
-    tst = (C.c_uint64 * (tcap * w))()
-    tact = (C.c_int32 * tcap)()
-    tlen = C.c_int32()
-    rc = lib.tlcg_run_node_trace(C.byref(m), C.byref(o), ranks, C.byref(st), lv, 65536, C.byref(n), tst, tact, tcap,
-                                 C.byref(tlen), err, 1024)
-    if rc != 0:
-        raise RuntimeError(f"tlcg_run_node: {err.value.decode()} ({rc})")
-    status = STATUS[st.status]
-    r = Result(status=status, generated=st.generated, distinct=st.distinct, depth=st.depth,
-               left_on_queue=0 if status == "ok" else st.frontier, levels=[lv[i] for i in range(n.value)],
-               collision_optimistic=st.fp_collision_optimistic, kernel_ms=st.kernel_ms, expand_ms=st.expand_ms,
-               levels_redone=st.levels_redone, engine={v: k for k, v in ENGINES.items()}.get(st.engine, "?"),
-               host_states=st.host_states, fpset_host_states=st.fpset_host_states,
-               transport={1: "local", 2: "rccl"}.get(st.transport, ""))
-    if st.invariant >= 0:
-        r.invariant = model.invariants[st.invariant]
-    if st.action >= 0:
-        r.action = ACTIONS[st.action]
-    r.trace = [("Init" if tact[i] < 0 else ACTIONS[tact[i]], _from_words(tst, i, w))
-               for i in range(min(tlen.value, tcap))]
-    return r
+    return o
+
+
+class Node:
+    """The ranks of one node kept across checks (tlcg_node_create / run /
+    destroy): rank r on device r mod device_count, driven by one host thread
+    each; the contexts (FPSet shards, stores, outboxes) and the transport are
+    built once, so run() costs the level loop only.  run() returns what
+    run_node returns."""
+
+    def __init__(self, model: Model, ranks: int, **opts):
+        self.lib = load_library()
+        self.model = model
+        self._m = model.to_c()  # (kept alive: the contexts copy it, user_defs included)
+        self.node = C.c_void_p()
+        err = C.create_string_buffer(1024)
+        rc = self.lib.tlcg_node_create(C.byref(self._m), C.byref(_node_opts(**opts)), ranks, C.byref(self.node),
+                                       err, 1024)
+        if rc != 0:
+            raise RuntimeError(f"tlcg_node_create: {err.value.decode()} ({rc})")
+
+    def run(self) -> Result:
+        model, lib = self.model, self.lib
+        st = tlcg_stats()
+        lv = (C.c_uint64 * 65536)()
+        n = C.c_int32()
+        err = C.create_string_buffer(1024)
+        w = state_words(model)
+        tcap = 4096
+        tst = (C.c_uint64 * (tcap * w))()
+        tact = (C.c_int32 * tcap)()
+        tlen = C.c_int32()
+        rc = lib.tlcg_node_run(self.node, C.byref(st), lv, 65536, C.byref(n), tst, tact, tcap, C.byref(tlen), err, 1024)
+        if rc != 0:
+            raise RuntimeError(f"tlcg_node_run: {err.value.decode()} ({rc})")
+        status = STATUS[st.status]
+        r = Result(status=status, generated=st.generated, distinct=st.distinct, depth=st.depth,
+                   left_on_queue=0 if status == "ok" else st.frontier, levels=[lv[i] for i in range(n.value)],
+                   collision_optimistic=st.fp_collision_optimistic, kernel_ms=st.kernel_ms, expand_ms=st.expand_ms,
+                   levels_redone=st.levels_redone, engine={v: k for k, v in ENGINES.items()}.get(st.engine, "?"),
+                   host_states=st.host_states, fpset_host_states=st.fpset_host_states,
+                   transport={1: "local", 2: "rccl"}.get(st.transport, ""))
+        if st.invariant >= 0:
+            r.invariant = model.invariants[st.invariant]
+        if st.action >= 0:
+            r.action = ACTIONS[st.action]
+        r.trace = [("Init" if tact[i] < 0 else ACTIONS[tact[i]], _from_words(tst, i, w))
+                   for i in range(min(tlen.value, tcap))]
+        return r
+
+    def close(self):
+        if self.node:
+            self.lib.tlcg_node_destroy(self.node)
+            self.node = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
+
+
+def run_node(model: Model, ranks: int, device: int = 0, log2_fpset_slots: int = 0, state_capacity: int = 0,
+             partition: int = 0, engine: str = "auto", spill: bool = False, device_store_cap: int = 0,
+             fpset_spill: bool = False, log2_fpset_max: int = 0) -> Result:
+    """The check by this one process on `ranks` contexts, rank r on device
+    r mod device_count (tlcg_node_create + tlcg_node_run; `tlc-hip -gpus N`).
+    On an error .trace is the counterexample walked across the ranks' stores
+    (a shortest one; TLC -workers 1's own trace: Checker(..., tlc_order=True))."""
+    node = Node(model, ranks, device=device, log2_fpset_slots=log2_fpset_slots, state_capacity=state_capacity,
+                partition=partition, engine=engine, spill=spill, device_store_cap=device_store_cap,
+                fpset_spill=fpset_spill, log2_fpset_max=log2_fpset_max)
+    try:
+        return node.run()
+    finally:
+        node.close()

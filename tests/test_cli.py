@@ -166,6 +166,28 @@ def test_injected_invariant_outside_the_subset_is_refused(tmp_path):
     assert rc == 150
 
 
+def test_builtin_module_definition_without_text_is_refused(tmp_path):
+    """built-in module mode (no .tla) with -defs: an INVARIANT naming one of
+    the module's own definitions whose text the binary does not hold (Init)
+    is refused with TLC's config error, never bound to a -defs definition"""
+    defs = tmp_path / "added.tla"
+    defs.write_text("ContextBound == compactedTopicContext < 3\n")
+    cfg = tmp_path / "m.cfg"
+    cfg.write_text(numeric_cfg(INVARIANTS="Init"))
+    p = subprocess.run([CLI, "-config", str(cfg), "-defs", str(defs)], capture_output=True, text=True, timeout=60,
+                       cwd=str(tmp_path))
+    out = p.stdout + p.stderr
+    assert "invariant Init cannot be checked: its definition text is not available" in out
+    assert "Computing initial states" not in out
+    assert p.returncode == 151
+    # the -defs definition itself is still bound
+    cfg.write_text(numeric_cfg(INVARIANTS="ContextBound"))
+    p = subprocess.run([CLI, "-config", str(cfg), "-defs", str(defs)], capture_output=True, text=True, timeout=60,
+                       cwd=str(tmp_path))
+    out = p.stdout + p.stderr
+    assert "Computing initial states..." in out
+
+
 @needs_ref
 def test_edited_spec_invariant_becomes_a_user_invariant(tmp_path):
     """an edited CompactionHorizonCorrectness is checked from its new text, not refused"""

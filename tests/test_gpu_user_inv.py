@@ -2,7 +2,11 @@
 injected into compaction.tla, violated at depth) against the Python oracle's
 fixtures (tests/golden/user_inv.json, oracle/tla_eval.py): verdict, the
 violated invariant, depth, counts, TLC's counterexample trace text and TLC's
-counters at its stop point.  The invariants run in k_user_check on the GPU."""
+counters at its stop point.  The global engine runs them in k_user_check;
+the on-chip engines (component, component tree) run them as device code
+generated from the compiled program (user_inv.cpp user_device_source) inside
+their hipRTC-specialized kernels; the ranks of a multi-GPU check run them in
+whichever engine each rank uses."""
 import json
 import os
 
@@ -21,12 +25,22 @@ def model(case):
     return tlcgpu.Model(invariants=tuple(g["invariants"]), user_defs=g["user_defs"], **g["constants"])
 
 
+def check_path(m, r, want):
+    """some shortest counterexample: a path of the spec ending in a violating state"""
+    assert r.trace[0][0] == "Init" and len(r.trace) == want["depth"]
+    for (_, s), (a, t) in zip(r.trace, r.trace[1:]):
+        assert (a, t) in tlcgpu.host_successors(m, s)
+    c = tlcgpu.host_check_invariants(m, r.trace[-1][1])
+    assert c >= 0 and m.invariants[c >> 1] == want["invariant"]
+
+
 @pytest.mark.parametrize("order", ["tlc_order", "fast"])
 @pytest.mark.parametrize("case", sorted(GOLD))
 def test_user_invariant_check(case, order):
+    """the global engine (TLC order, or forced): k_user_check on every level"""
     m = model(case)
     want = GOLD[case]["result"]
-    ck = tlcgpu.Checker(m, tlc_order=order == "tlc_order")
+    ck = tlcgpu.Checker(m, tlc_order=order == "tlc_order", engine="global")
     r = ck.run()
     assert r.engine == "global"
     assert r.status == want["result"], (case, r.status)
@@ -45,30 +59,112 @@ def test_user_invariant_check(case, order):
         # TLC's "X states generated, Y distinct states found, Z states left on queue" at its stop
         assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"])
     else:
-        # some shortest counterexample: a path of the spec ending in a violating state
-        assert r.trace[0][0] == "Init" and len(r.trace) == want["depth"]
-        for (_, s), (a, t) in zip(r.trace, r.trace[1:]):
-            assert (a, t) in tlcgpu.host_successors(m, s)
-        c = tlcgpu.host_check_invariants(m, r.trace[-1][1])
-        assert c >= 0 and m.invariants[c >> 1] == want["invariant"]
+        check_path(m, r, want)
     ck.close()
 
 
-def test_user_invariants_refuse_other_engines_and_ranks():
-    m = model("U_LedgerCount")
-    for kw in (dict(engine="component"), dict(engine="tree"), dict(world=2)):
-        with pytest.raises(RuntimeError):
-            tlcgpu.Checker(m, **kw)
+@pytest.mark.parametrize("case", sorted(GOLD))
+def test_user_invariant_on_chip(case):
+    """the default engine: the component engine without a Producer (its lanes
+    keep TLC's order, so a violation's trace is TLC's -workers 1 trace), the
+    component tree with one (an error there is reported by the global engine's
+    re-run); the user invariants evaluated inside the specialized kernels"""
+    m = model(case)
+    want = GOLD[case]["result"]
+    # (C = 5, K = 2: 302 states per component, past a lane's 255: the tree's closed mode)
+    on_chip = "tree" if m.model_producer or case == "U_C5K2_MaxLedgerBound" else "component"
+    ck = tlcgpu.Checker(m)
+    r = ck.run()
+    assert r.status == want["result"], (case, r.status)
+    if want["result"] == "ok":
+        assert r.engine == on_chip
+        assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                                 want["levels"])
+        ck.close()
+        return
+    assert r.engine == ("global" if on_chip == "tree" else "component")
+    assert r.depth == want["depth"]
+    assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+    if want["result"] in ("invariant", "invariant_error"):
+        assert r.invariant == want["invariant"]
+    if on_chip == "component":
+        assert [a for a, _ in r.trace] == [t["action"] for t in want["trace"]]
+        assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
+    else:
+        check_path(m, r, want)
+    ck.close()
+
+
+@pytest.mark.parametrize("case", ["U_LedgerCount", "U_all_hold", "U_ContextLedgerError", "U_mixed_user_first",
+                                  "U_C5_ContextBound"])
+def test_user_invariant_tree_closed_mode(case):
+    """the component tree's closed mode (components past a lane of the
+    component engine) with the user invariants in its kernel: counts of an
+    error-free check; an error is reported by the global engine's re-run"""
+    m = model(case)
+    want = GOLD[case]["result"]
+    r = tlcgpu.run(m, engine="tree")
+    assert r.status == want["result"], (case, r.status)
+    if want["result"] == "ok":
+        assert r.engine == "tree"
+        assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                                 want["levels"])
+    else:
+        assert r.engine == "global" and r.depth == want["depth"]
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+        check_path(m, r, want)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", sorted(GOLD))
+def test_user_invariant_ranks(case, world):
+    """world 2 / 3 ranks on one GPU (tlcg_run_node): each rank's engine checks
+    the user invariants on its share; the combined verdict, depth and
+    end-of-level counts are the one-rank ones, and the trace walked across the
+    ranks is a counterexample of the spec"""
+    m = model(case)
+    want = GOLD[case]["result"]
+    r = tlcgpu.run_node(m, world)
+    assert r.status == want["result"], (case, r.status)
+    if want["result"] == "ok":
+        assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                                 want["levels"])
+        return
+    assert r.depth == want["depth"]
+    assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+    if want["result"] in ("invariant", "invariant_error"):
+        assert r.invariant == want["invariant"]
+        check_path(m, r, want)
+
+
+@pytest.mark.parametrize("case", ["U_LedgerCount", "U_all_hold", "U_ContextLedgerError", "U_producer_LedgerCount"])
+def test_user_invariant_open_partition(case):
+    """partition 2 (the whole state: successors cross ranks, BASELINE config
+    4): the user invariants on every rank's new level, absorbed states
+    included (tlcg_end_level)"""
+    m = model(case)
+    want = GOLD[case]["result"]
+    r = tlcgpu.run_node(m, 3, partition=2, engine="global")
+    assert r.status == want["result"], (case, r.status)
+    assert r.depth == want["depth"]
+    if want["result"] == "ok":
+        assert (r.generated, r.distinct, r.levels) == (want["generated"], want["distinct"], want["levels"])
+    else:
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+        if want["result"] in ("invariant", "invariant_error"):
+            check_path(m, r, want)
 
 
 def test_user_invariant_at_scale():
-    """M8 (1.1e8 states) with an invariant that holds everywhere and one that
-    fails at depth 12: the check kernel runs on every level of the global engine"""
+    """M8 (1.1e8 states) with an invariant that holds everywhere (the
+    component engine) and one that fails at depth 12 (TLC order: the global
+    engine's check kernel on every level)"""
     g = GOLD["U_all_hold"]
     keys = range(1, 11)
     m = tlcgpu.Model(key_space=keys, value_space=keys, invariants=tuple(g["invariants"]), user_defs=g["user_defs"])
     r = tlcgpu.Checker(m, state_capacity=120_000_000).run(with_trace=False)
     assert (r.status, r.generated, r.distinct, r.depth) == ("ok", 147_039_563, 109_836_782, 20)
+    assert r.engine == "component"
     g = GOLD["U_LedgerCount"]
     m = tlcgpu.Model(key_space=keys, value_space=keys, invariants=tuple(g["invariants"]), user_defs=g["user_defs"])
     r = tlcgpu.Checker(m, tlc_order=True, state_capacity=120_000_000).run()

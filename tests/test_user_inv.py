@@ -144,3 +144,55 @@ def test_bulleted_lists_are_read_by_column():
 def test_user_definition_shadows_a_spec_invariant_name():
     m = T.Model(invariants=("TypeSafe",), user_defs={"TypeSafe": "FALSE"})
     assert T.host_check_invariants(m, T.host_init_state(m, 0)) == 0
+
+
+def _golden_user():
+    import json
+    return json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "user_inv.json")))
+
+
+def _golden_model(case):
+    g = _golden_user()[case]
+    return T.Model(invariants=tuple(g["invariants"]), user_defs=g["user_defs"], **g["constants"])
+
+
+@pytest.mark.parametrize("case", ["U_all_hold", "U_LedgerCount", "U_ArithCase", "U_C5K2_MaxLedgerBound",
+                                  "U_producer_LedgerCount", "U_KeysKnown"])
+def test_user_invariants_compile_into_the_specialized_kernels(case):
+    """the program lowered to device code (user_inv.cpp user_device_source)
+    compiles with the component and tree kernels for gfx950 without a device
+    (a failure would leave the model to the global engine at run time)"""
+    import ctypes as C
+    m = _golden_model(case).to_c()
+    err = C.create_string_buffer(8192)
+    n = T.load_library().tlcg_jit_selftest(C.byref(m), b"gfx950", err, 8192)
+    assert n > 0, err.value.decode()[:3000]
+
+
+def test_user_invariant_views_agree_on_every_reachable_state():
+    """the on-chip engines evaluate a user invariant on their own encoding
+    (component_code.h UVCode: a component code plus the component's
+    constants); on every reachable state of 200 components of each
+    non-producer golden cfg, every field it reads and every invariant's
+    outcome equal the packed word's (model.h UVWord), narrow and wide"""
+    for case, g in sorted(_golden_user().items()):
+        m = _golden_model(case)
+        if m.model_producer:
+            continue
+        assert T.host_component_selfcheck(m, 0, 200) > 0, case
+    wide = T.Model(invariants=("LedgerCount",), user_defs={"LedgerCount": CASES["LedgerCount"]},
+                   compaction_times_limit=12, key_space=range(1, 4), value_space=range(1, 4))
+    assert T.state_words(wide) == 2 and T.host_component_selfcheck(wide, 0, 12) > 0
+
+
+def test_integer_overflow_is_an_evaluation_error():
+    """TLC's integers are 32-bit: an arithmetic result outside -2^31..2^31-1
+    is an evaluation error ([TLC-ext] the overflow check of TLC's Naturals /
+    Integers), never a wrapped or 64-bit value; parity unpinned against TLC"""
+    s = T.host_init_state(T.Model(), 0)
+    big = T.Model(invariants=("Big",), user_defs={"Big": "2147483647 + crashTimes + 1 > 0"})
+    assert T.host_check_invariants(big, s) == 1  # (index 0 << 1) | error
+    ok = T.Model(invariants=("Fits",), user_defs={"Fits": "2147483646 + crashTimes + 1 > 0"})
+    assert T.host_check_invariants(ok, s) == -1
+    mul = T.Model(invariants=("Mul",), user_defs={"Mul": "65536 * 65536 + crashTimes >= 0"})
+    assert T.host_check_invariants(mul, s) == 1
