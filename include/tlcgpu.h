@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TLCG_ABI_VERSION 3
+#define TLCG_ABI_VERSION 4
 #define TLCG_MAX_SET 63 /* largest KeySpace / ValueSpace */
 #define TLCG_MAX_INV 8
 
@@ -169,6 +169,10 @@ typedef struct tlcg_stats {
   uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
   uint64_t fpset_host_states; /* states held by the host FPSet tier (tlcg_opts.fpset_spill) */
   uint64_t transport;        /* multi-rank runs: 1 host threads + device copies, 2 RCCL; 0 one context */
+  uint64_t tlc_exact;        /* 1: the run stopped on an error and its trace (tlcg_trace_words) and
+                                tlcg_tlc_stop_stats are TLC -workers 1's: a TLC-order run (also the
+                                one a component-tree error switches to on one rank), or an on-chip
+                                engine's error on a closed partition (one rank) */
 } tlcg_stats;
 
 typedef struct tlcg_ctx tlcg_ctx;

@@ -785,6 +785,20 @@ struct tlcg_ctx {
   uint32_t tree_disp_mult = 0;               // the tree's closed-mode slot displacements (build_slot_disp)
   uint16_t tree_disp[TREE_DISP] = {};
   bool no_tree = false;                   // the ranks fell back from the sharded component tree (run_ranks)
+  bool tree_event = false;                // the last tree run raised an error (Producer modelled: TLC order reports it)
+  bool tlc_switched = false;              // this run took TLC order for a tree error (opts.tlc_order restored at tlcg_init)
+  u64 range_hi = 0;                       // closed, one rank: run only initial states [0, range_hi) (TLC stop statistics)
+  u64 ev_comp = ~0ull;                    // closed partitions, on-chip engines: the initial state of the error's component
+  // a run whose level 0 is one given state instead of Init (the Producer
+  // tree's error report: a TLC-order run over one subtree, producer_error)
+  bool seed_valid = false;
+  u128 seed_state = 0;
+  // TLC's stop statistics worked out with the run (the Producer tree's error report)
+  bool stop_cached = false;
+  u64 stop_g = 0, stop_d = 0, stop_q = 0;
+  // the component tree's layout (Producer modelled, one rank): per layer, the
+  // global index of its first chunk and of its first component
+  std::vector<u64> tree_layer_gbase, tree_layer_cbase;
   bool tree_codes = false;                // the store holds the tree's closed-mode component codes (tree_body.h)
   u64 tree_r0 = 0;                        //   of the components of initial states tree_r0, tree_r0 + 1, ..
   UserProg* d_prog = nullptr;            // the user invariants' program on the device (user_inv.h)
@@ -1200,7 +1214,7 @@ bool for_each_stored(tlcg_ctx* c, u64 g0, u64 g1, F&& fn) {
 // (re)build the FPSet at 2^log2 slots holding the stored states [t0_base, n)
 // (with the host FPSet tier, older states are in the host runs)
 bool rebuild_fpset(tlcg_ctx* c, int log2, u64 n) {
-  if (log2 != c->log2 || !c->d_slots) {
+  if (log2 != c->log2 || !c->d_slots || (c->opts.tlc_order && !c->d_dkey_slot)) {
     hipFree(c->d_slots);
     c->d_slots = nullptr;
     hipFree(c->d_dkey_slot);
@@ -1635,6 +1649,11 @@ void fill_stats(tlcg_ctx* c, tlcg_stats* st) {
   st->kernel_ms = c->kernel_ms;
   st->expand_ms = c->expand_ms;
   st->levels_redone = c->levels_redone;
+  // the trace and tlcg_tlc_stop_stats are TLC -workers 1's: a TLC-order run,
+  // or an on-chip engine's error on a closed partition (one rank)
+  st->tlc_exact = c->status >= TLCG_VIOLATION && c->opts.world == 1 &&
+                  ((c->engine == TLCG_ENGINE_GLOBAL && c->opts.tlc_order) || c->stop_cached ||
+                   (c->engine != TLCG_ENGINE_GLOBAL && !c->hm.L.producer && c->ev_comp != ~0ull));
 }
 
 // the state word of store slot g holding a component code (the tree's closed
@@ -1777,6 +1796,7 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
   const int kind = (int)((ev >> 4) & 3);
   c->ev_word = ev;
   c->ev_level = level;
+  c->ev_comp = idx0;
   switch (kind) {
     case EVK_VIOLATION: c->status = TLCG_VIOLATION; break;
     case EVK_INV_ERROR: c->status = TLCG_INVARIANT_ERROR; break;
@@ -1826,6 +1846,144 @@ bool resolve_comp_event(tlcg_ctx* c, u64 ev) {
     c->ev_action = action;
   }
   return true;
+}
+
+// ---- TLC's one-worker run on one component of a closed partition ----
+//
+// Without a Producer the reachable graph is the disjoint union of one
+// component per initial state, and TLC's FIFO queue holds every level in the
+// Init order of the components, then each component's own FIFO order (level
+// 0 is in Init order and successors never leave their component).  So TLC's
+// first error lies in the least component with an error at the least error
+// level E, and is that component's own first error: the host replays just
+// that component (<= a few thousand states) in TLC's worker order
+// (ModelChecker.doNext, [TLC-ext]: FIFO states, Next disjuncts in order, each
+// action's successors counted before any is checked, the run stopping at the
+// first violating new state, a failing action or after a deadlocked state's
+// actions), which gives the trace and the component's share of TLC's stop
+// counters.  The on-chip engines then report TLC's error without a
+// global-engine re-run.
+struct CompReplay {
+  int status = TLCG_DONE, invariant = -1, action = -1, kind = -1;
+  int level = -1;              // E: the violating state's level, or the failing / deadlocked state's + 1
+  std::vector<u128> trace;     // Init .. the violating (or the failing) state
+  std::vector<int> acts;
+  u64 p_index = 0;             // the stopping state p's position in the component's level E - 1
+  u64 outdeg_before = 0;       // out-degrees of the component's level-(E - 1) states before p
+  u64 partial = 0;             // p's successors counted before the stop
+  u64 found_next = 0;          // the component's level-E states discovered by the stop (the violating one too)
+};
+
+int check_any(const tlcg_ctx* c, u128 s) {
+  return c->words == 2 ? host_check_all<u128>(c->hm, s) : host_check_all<u64>(c->hm, (u64)s);
+}
+
+// false when the component holds no error (the caller's event was not this component's)
+bool replay_component(const tlcg_ctx* c, u64 idx0, CompReplay* out) {
+  const Layout& L = c->hm.L;
+  struct H {
+    size_t operator()(u128 x) const { return (size_t)mix64((u64)x ^ mix64((u64)(x >> 64) + 0x9E3779B97F4A7C15ull)); }
+  };
+  std::unordered_map<u128, uint32_t, H> seen;
+  std::vector<u128> q;
+  std::vector<int32_t> par, act, lvl;
+  const u128 s0 = c->words == 2 ? init_state<u128>(L, idx0) : (u128)init_state<u64>(L, idx0);
+  auto chain = [&](int64_t i, CompReplay* r) {  // Init .. state i
+    for (int64_t j = i; j >= 0; j = par[(size_t)j]) {
+      r->trace.push_back(q[(size_t)j]);
+      r->acts.push_back(par[(size_t)j] < 0 ? TLCG_ACT_INIT : act[(size_t)j]);
+    }
+    std::reverse(r->trace.begin(), r->trace.end());
+    std::reverse(r->acts.begin(), r->acts.end());
+  };
+  q.push_back(s0);
+  par.push_back(-1);
+  act.push_back(TLCG_ACT_INIT);
+  lvl.push_back(0);
+  seen.emplace(s0, 0u);
+  const int c0 = check_any(c, s0);
+  if (c0 >= 0) {
+    out->status = (c0 & 1) ? TLCG_INVARIANT_ERROR : TLCG_VIOLATION;
+    out->kind = (c0 & 1) ? EVK_INV_ERROR : EVK_VIOLATION;
+    out->invariant = c0 >> 1;
+    out->action = TLCG_ACT_INIT;
+    out->level = 0;
+    chain(0, out);
+    return true;
+  }
+  const int nord = L.nkv + N_ACTIONS - 1;  // Next ordinals (compaction.tla:216-231)
+  int64_t lvl_start = 0, cur_level = 0;
+  u64 outdeg_sum = 0, next_found = 0;
+  for (size_t head = 0; head < q.size(); ++head) {
+    const u128 p = q[head];
+    if (lvl[head] != cur_level) {  // a new level is dequeued
+      cur_level = lvl[head];
+      lvl_start = (int64_t)head;
+      outdeg_sum = 0;
+      next_found = 0;
+    }
+    u64 gen = 0;
+    auto stop = [&](int status, int kind, int action, int inv, int64_t last) {
+      out->status = status;
+      out->kind = kind;
+      out->action = action;
+      out->invariant = inv;
+      out->level = (int)cur_level + 1;
+      out->p_index = (u64)((int64_t)head - lvl_start);
+      out->outdeg_before = outdeg_sum;
+      out->partial = gen;
+      out->found_next = next_found;
+      chain(last, out);
+      return true;
+    };
+    for (int o = 0; o < nord;) {
+      // one action's successors: the Producer's (key, value) pairs, or one disjunct
+      const int a = action_of_ordinal(L, o);
+      const int o1 = a == ACT_PRODUCER ? L.nkv : o + 1;
+      std::vector<u128> ts;
+      for (; o < o1; ++o) {
+        u128 t = 0;
+        const int r = successor_at_any(c, p, o, &t);
+        if (r == 2) return stop(TLCG_ACTION_ERROR, EVK_ACTION_ERROR, a, -1, (int64_t)head);
+        if (r == 1) ts.push_back(t);
+      }
+      gen += ts.size();  // counted as one StateVec before any is put and checked
+      for (const u128 t : ts) {
+        if (seen.count(t)) continue;
+        seen.emplace(t, (uint32_t)q.size());
+        q.push_back(t);
+        par.push_back((int32_t)head);
+        act.push_back(a);
+        lvl.push_back((int32_t)cur_level + 1);
+        ++next_found;
+        const int ci = check_any(c, t);
+        if (ci >= 0)
+          return stop((ci & 1) ? TLCG_INVARIANT_ERROR : TLCG_VIOLATION, (ci & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
+                       a, ci >> 1, (int64_t)q.size() - 1);
+      }
+    }
+    if (!gen && L.check_deadlock) return stop(TLCG_DEADLOCK, EVK_DEADLOCK, -1, -1, (int64_t)head);
+    outdeg_sum += gen;
+    if (q.size() > (1u << 24)) return false;  // (not a component of a closed partition)
+  }
+  return false;
+}
+
+// the context's error from a replay of component `comp`: verdict, event
+// (as the component engine's key, for fill_stats) and the trace
+void set_replay_event(tlcg_ctx* c, u64 comp, const CompReplay& rp) {
+  c->status = rp.status;
+  c->ev_level = rp.level;
+  c->ev_comp = comp;
+  c->ev_word = make_comp_event(rp.level, comp, 0, rp.action < 0 ? 15 : rp.action, rp.kind,
+                               rp.invariant < 0 ? 0 : rp.invariant);
+  c->ev_action = rp.action;
+  c->ev_state = rp.trace.back();
+  c->ev_parent_gidx = NO_PARENT;
+  c->ev_parent_ref = NO_PARENT;
+  c->xtrace_states = rp.trace;
+  c->xtrace_acts = rp.acts;
+  c->xtrace_valid = true;
 }
 
 // ---- component engine (component.h) ----
@@ -1893,7 +2051,8 @@ int run_component(tlcg_ctx* c) {
   const Layout& L = hm.L;
   const int mb = L.msg_sh + L.N * L.mw;
   const u64 W = (u64)c->opts.world, R = (u64)c->opts.rank;
-  const u64 r0 = hm.n_init * R / W, r1 = hm.n_init * (R + 1) / W;
+  const u64 r0 = c->range_hi ? 0 : hm.n_init * R / W;
+  const u64 r1 = c->range_hi ? std::min<u64>(c->range_hi, hm.n_init) : hm.n_init * (R + 1) / W;
   c->engine = TLCG_ENGINE_COMPONENT;
   c->passes.clear();
   c->comp_levels.assign(COMP_MAXLV, 0);
@@ -2074,6 +2233,190 @@ bool tree_closed_applicable(const tlcg_ctx* c) {
          !(c->hm.user && (jit_off() || L.msgs_mask_hi));
 }
 
+// ---- the Producer tree's error, reported as TLC reports it ----
+//
+// TLC's queue order is the lexicographic order of each state's least
+// shortest path from Init, as the sequence of Next ordinals it takes (a
+// level is sorted by its states' first discoverers, which are sorted the
+// same way).  The Producer's successors have the least ordinals
+// (compaction.tla:216-219: its disjunct comes first, one ordinal per
+// message), and BrokerCrash, the only other action enabled while
+// `messages` is empty (CompactorPhaseOne needs Len(messages) > 0, :95),
+// reads no message and commutes with it.  So every state whose
+// `messages` starts with message m -- the component subtree m -- has a
+// shortest path that produces m first, its least path starts with
+// ordinal m, and TLC's queue holds every level >= 1 as subtree 0,
+// subtree 1, .., then the states of the empty `messages` (the root).  The
+// first error lies in the least subtree with an error at the least error
+// level E, which the tree's kernel reports (tree_event_key); a TLC-order
+// run of that subtree alone -- level 0 its seed state (message m produced
+// from Init), levels up to E -- finds TLC's first error, its trace and its
+// share of TLC's stop counters, and the tree's counts give the rest.  The
+// subtree run's level sizes must equal the tree's depth histogram of the
+// subtree (a state reached deeper than its depth would show at its own
+// depth as a missing state), which checks the argument on the run itself;
+// the subtrees before the erroring one (rarely any) are run to level E the
+// same way.  Returns 1 reported, 0 the global engine must report it, -1 error.
+namespace {
+
+// the tree's depth histogram of subtree m (levels 0..maxd), from the depth bytes of its chunks
+bool subtree_depths(tlcg_ctx* c, u64 m, int maxd, std::vector<u64>* hist) {
+  const Layout& L = c->hm.L;
+  hist->assign((size_t)maxd + 1, 0);
+  const u64 cap = (u64)c->tree_cap;
+  u64 per = 1;  // components of subtree m in layer l: [m * per, (m + 1) * per), per = nkv^(l - 1)
+  for (int l = 1; l <= L.N && (size_t)l < c->tree_layer_gbase.size(); ++l, per *= (u64)L.nkv) {
+    const u64 c0 = m * per;
+    std::vector<uint32_t> n(per);
+    std::vector<uint8_t> dep(per * cap);
+    HIPCHK(hipMemcpy(n.data(), c->d_tree_n + c->tree_layer_cbase[(size_t)l] + c0, per * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(dep.data(), c->d_tree_dep + c->tree_layer_gbase[(size_t)l] + c0 * cap, per * cap,
+                     hipMemcpyDeviceToHost));
+    for (u64 i = 0; i < per; ++i)
+      for (u64 k = 0; k < n[i] && k < cap; ++k)
+        if (dep[i * cap + k] <= maxd) ++(*hist)[dep[i * cap + k]];
+  }
+  return true;
+}
+
+// a TLC-order run of subtree m to level E (absolute; its level r is level r + 1):
+// the context, stopped on an error or after level E; nullptr on failure
+tlcg_ctx* subtree_run(tlcg_ctx* c, u64 m, int E) {
+  const Layout& L = c->hm.L;
+  tlcg_opts o = c->opts;
+  o.world = 1;
+  o.rank = 0;
+  o.engine = TLCG_ENGINE_GLOBAL;
+  o.tlc_order = 1;
+  o.outdegree = 0;
+  o.state_capacity = 0;
+  o.log2_fpset_slots = 0;
+  o.fpset_spill = 0;
+  o.device_store_cap = 0;
+  tlcg_model md = c->model;
+  tlcg_ctx* t = nullptr;
+  if (tlcg_create(&md, &o, &t) != 0) {
+    tlcg_destroy(t);
+    return nullptr;
+  }
+  t->seed_valid = true;
+  t->seed_state = producer_succ<u64>(L, init_state<u64>(L, 0), 0, (int)m);
+  tlcg_stats st;
+  if (tlcg_init(t, &st) != 0) {
+    tlcg_destroy(t);
+    return nullptr;
+  }
+  while (t->status == TLCG_RUNNING && (int)t->level_base.size() - 1 < E)
+    if (tlcg_step_level(t, &st) != 0) {
+      tlcg_destroy(t);
+      return nullptr;
+    }
+  return t;
+}
+
+// the run's level sizes (relative levels 0..k) against the tree's depths 1..k + 1 of the subtree
+bool subtree_run_matches(tlcg_ctx* c, tlcg_ctx* t, u64 m, int E) {
+  std::vector<u64> hist;
+  if (!subtree_depths(c, m, E, &hist)) return false;
+  for (int r = 0; r + 1 <= E; ++r) {
+    const u64 got = (size_t)r + 1 < t->level_base.size() ? t->level_base[(size_t)r + 1] - t->level_base[(size_t)r] : 0;
+    if (got != hist[(size_t)r + 1]) return false;
+  }
+  return true;
+}
+
+int producer_error(tlcg_ctx* c, u64 evk) {
+  const Layout& L = c->hm.L;
+  const int E = (int)(evk >> 40);
+  const u64 sub = evk & ((1ull << 40) - 1);
+  if (E < 2 || sub >= (u64)L.nkv || sub > 8 || c->words != 1 || c->hm.n_init != 1) return 0;
+  // the subtrees before: no error up to level E (sub is the least with one); their levels E - 1, E
+  u64 pre_lm1 = 0, pre_l = 0, pre_gen = 0;
+  for (u64 m = 0; m < sub; ++m) {
+    tlcg_ctx* t = subtree_run(c, m, E);
+    if (!t) return 0;
+    const bool ok = t->status == TLCG_RUNNING || t->status == TLCG_DONE;
+    std::vector<u64> lg(4096);
+    int32_t ng = 0;
+    const bool good = ok && subtree_run_matches(c, t, m, E) && tlcg_level_generated(t, lg.data(), 4096, &ng) == 0;
+    if (good) {
+      auto lv = [&](int r) -> u64 {
+        return (size_t)r + 1 < t->level_base.size() ? t->level_base[(size_t)r + 1] - t->level_base[(size_t)r] : 0;
+      };
+      pre_lm1 += lv(E - 2);
+      pre_l += lv(E - 1);
+      pre_gen += E - 1 < ng ? lg[(size_t)E - 1] : 0;  // (lg[k]: generated by expanding relative level k - 1)
+    }
+    tlcg_destroy(t);
+    if (!good) return 0;
+  }
+  tlcg_ctx* t = subtree_run(c, sub, E);
+  if (!t) return 0;
+  int res = 0;
+  uint64_t g = 0, d = 0, q = 0;
+  std::vector<uint64_t> tst(4096);
+  std::vector<int32_t> tact(4096);
+  int32_t tn = 0;
+  tlcg_stats ts;
+  if (t->status >= TLCG_VIOLATION && t->ev_level == E - 1 && subtree_run_matches(c, t, sub, E) &&
+      tlcg_tlc_stop_stats(t, &g, &d, &q) == 0 && tlcg_trace_words(t, tst.data(), tact.data(), 4096, &tn) == 0 &&
+      tn >= 1 && tn < 4096) {
+    fill_stats(t, &ts);
+    auto lv = [&](int r) -> u64 {
+      return (size_t)r + 1 < t->level_base.size() ? t->level_base[(size_t)r + 1] - t->level_base[(size_t)r] : 0;
+    };
+    // the subtree run's share at its stop (p: the stopping state, relative level E - 2)
+    u64 below = 0, upto = 0;  // its states in levels < E - 2, <= E - 2
+    for (int r = 0; r < E - 1; ++r) (r < E - 2 ? below : upto) += lv(r);
+    upto += below;
+    const u64 within = g - t->gen_at[(size_t)E - 2];   // level E - 2's out-degrees before p, and p's counted ones
+    const u64 found = d - upto;                         // level E - 1 states found by the stop
+    const u64 rank = (d - q - 1) - below;               // p's place in its level
+    // the whole model: the tree's full levels, the subtrees before, the share
+    auto at = [](const std::vector<u64>& v, int i) -> u64 { return i >= 0 && (size_t)i < v.size() ? v[(size_t)i] : 0; };
+    u64 gen = c->comp_init, dist = 0, pos = 0;
+    for (int l = 0; l < E - 1; ++l) {
+      gen += at(c->comp_level_gen, l);
+      pos += at(c->comp_levels, l);
+    }
+    for (int l = 0; l <= E - 1; ++l) dist += at(c->comp_levels, l);
+    c->stop_g = gen + pre_gen + within;
+    c->stop_d = dist + pre_l + found;
+    c->stop_q = c->stop_d - (pos + pre_lm1 + rank + 1);
+    c->stop_cached = true;
+    // the verdict and TLC's trace: Init, the Producer's step to the seed, the subtree run's
+    c->status = t->status;
+    c->ev_level = E;
+    const int kind = t->status == TLCG_VIOLATION ? EVK_VIOLATION : t->status == TLCG_INVARIANT_ERROR ? EVK_INV_ERROR
+                   : t->status == TLCG_DEADLOCK ? EVK_DEADLOCK : EVK_ACTION_ERROR;
+    c->ev_word = make_comp_event(E, sub, 0, ts.action < 0 ? 15 : ts.action, kind, ts.invariant < 0 ? 0 : ts.invariant);
+    c->ev_action = ts.action;
+    c->ev_parent_gidx = NO_PARENT;
+    c->ev_parent_ref = NO_PARENT;
+    c->xtrace_states.assign(1, (u128)init_state<u64>(L, 0));
+    c->xtrace_acts.assign(1, TLCG_ACT_INIT);
+    for (int i = 0; i < tn; ++i) {
+      c->xtrace_states.push_back((u128)tst[(size_t)i]);
+      c->xtrace_acts.push_back(i == 0 ? (int)ACT_PRODUCER : tact[(size_t)i]);
+    }
+    c->ev_state = c->xtrace_states.back();
+    c->xtrace_valid = true;
+    // the counts at the end of level E, as every engine reports them
+    if (c->comp_levels.size() > (size_t)E + 1) c->comp_levels.resize((size_t)E + 1);
+    c->comp_distinct = 0;
+    for (u64 x : c->comp_levels) c->comp_distinct += x;
+    c->comp_generated = c->comp_init;
+    for (size_t l = 0; l < (size_t)E && l < c->comp_level_gen.size(); ++l) c->comp_generated += c->comp_level_gen[l];
+    c->kernel_ms += t->kernel_ms;
+    c->expand_ms += t->expand_ms;
+    res = 1;
+  }
+  tlcg_destroy(t);
+  return res;
+}
+
+}  // namespace
+
 // Run the component tree.  Producer modelled: every layer, chunks of 384
 // states per component (the shipped N = 3, C = 3, K = 1 have at most 359),
 // then 1024 if one overflows.  Closed: this rank's components (a contiguous
@@ -2090,8 +2433,8 @@ int run_tree(tlcg_ctx* c) {
   const u64 W = (u64)c->opts.world, R = (u64)c->opts.rank;
   int shard = 0;  // Producer, W > 1: the layer whose components are split between the ranks
   if (closed) {
-    r0 = c->hm.n_init * R / W;
-    ncomp.push_back(c->hm.n_init * (R + 1) / W - r0);
+    r0 = c->range_hi ? 0 : c->hm.n_init * R / W;
+    ncomp.push_back(c->range_hi ? std::min<u64>(c->range_hi, c->hm.n_init) : c->hm.n_init * (R + 1) / W - r0);
     lbase.push_back(0);
   } else {
     // every component of layer l >= 1 lies in the subtree of one component of
@@ -2125,7 +2468,7 @@ int run_tree(tlcg_ctx* c) {
   u64 comps = 0;
   for (u64 x : ncomp) comps += x;
   if (!c->d_tree_ctr) {
-    const size_t bytes = sizeof(unsigned long long) * (2 * TREE_MAXLV * TREE_STRIPES + 2);
+    const size_t bytes = sizeof(unsigned long long) * (2 * TREE_MAXLV * TREE_STRIPES + 3);
     if (!alloc_bytes(c, (void**)&c->d_tree_ctr, bytes, "tree counters")) return -1;
     HIPCHK_I(hipHostMalloc((void**)&c->h_tree_ctr, bytes));
   }
@@ -2177,11 +2520,16 @@ int run_tree(tlcg_ctx* c) {
       c->tree_comps = comps;
     }
     unsigned long long* ctr = c->d_tree_ctr;
-    constexpr int kTreeCtr = 2 * TREE_MAXLV * TREE_STRIPES + 2;  // [stripe][lvl, lvl_gen], flags, max_n
-    HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * kTreeCtr, c->stream));
+    constexpr int kTreeCtr = 2 * TREE_MAXLV * TREE_STRIPES + 3;  // [stripe][lvl, lvl_gen], flags, max_n, event
+    HIPCHK_I(hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * (kTreeCtr - 1), c->stream));
+    HIPCHK_I(hipMemsetAsync(ctr + kTreeCtr - 1, 0xFF, sizeof(unsigned long long), c->stream));
     HIPCHK_I(hipEventRecord(c->e0, c->stream));
     u64 gbase = 0, cbase = 0, pgbase = 0, pcbase = 0;
+    c->tree_layer_gbase.clear();
+    c->tree_layer_cbase.clear();
     for (size_t l = 0; l < ncomp.size(); ++l) {
+      c->tree_layer_gbase.push_back(gbase);
+      c->tree_layer_cbase.push_back(cbase);
       TreeArgs a;
       a.L = L;
       a.layer = (int)l;
@@ -2205,6 +2553,7 @@ int run_tree(tlcg_ctx* c) {
       a.lvl_gen = ctr + TREE_MAXLV;
       a.flags = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV * TREE_STRIPES);
       a.max_n = reinterpret_cast<unsigned int*>(ctr + 2 * TREE_MAXLV * TREE_STRIPES + 1);
+      a.event = ctr + kTreeCtr - 1;
       a.stripe = 2 * TREE_MAXLV;
       a.nstripe = TREE_STRIPES;
       a.mult = closed ? c->tree_mult : DEFAULT_SLOT_MULT;
@@ -2232,8 +2581,12 @@ int run_tree(tlcg_ctx* c) {
     c->kernel_ms += ms;
     c->expand_ms += ms;
     const unsigned flags = (unsigned)c->h_tree_ctr[2 * TREE_MAXLV * TREE_STRIPES];
-    if (flags & TREE_EVENT) return 0;  // the global engine finds TLC's first error and its trace
+    if (flags & TREE_EVENT) {  // (Producer modelled) the global engine finds TLC's first error and its trace
+      c->tree_event = true;
+      return 0;
+    }
     if (flags & TREE_OVERFLOW) continue;
+    const u64 evk = c->h_tree_ctr[kTreeCtr - 1];  // closed mode: the least error key (tree_event_key)
     c->tree_cap = cap;
     // (the closed mode's store holds codes unless an A/B build asked for words)
     const char* jd = std::getenv("TLCG_JIT_DEFINES");
@@ -2269,6 +2622,35 @@ int run_tree(tlcg_ctx* c) {
     c->outdeg_valid = false;
     c->pending = 0;
     c->status = TLCG_DONE;
+    if (closed && evk != ~0ull) {
+      // TLC's first error: the least component with an error at the least
+      // level, replayed on the host in TLC's order (trace, event); the counts
+      // are those at the end of level E, as every engine reports them
+      const int E = (int)(evk >> 40);
+      const u64 comp = evk & ((1ull << 40) - 1);
+      CompReplay rp;
+      if (!replay_component(c, comp, &rp) || rp.level != E) {
+        c->err = "internal: the component tree's error was not found by its replay";
+        return -1;
+      }
+      set_replay_event(c, comp, rp);
+      if (c->comp_levels.size() > (size_t)E + 1) c->comp_levels.resize((size_t)E + 1);
+      c->comp_distinct = 0;
+      for (u64 x : c->comp_levels) c->comp_distinct += x;
+      c->comp_generated = c->comp_init;
+      for (size_t l = 0; l < (size_t)E && l < c->comp_level_gen.size(); ++l) c->comp_generated += c->comp_level_gen[l];
+    } else if (!closed && evk != ~0ull) {
+      // Producer modelled: TLC's first error from the one subtree holding it
+      // (producer_error); else (several ranks, an error of the root
+      // component or at level 0 / 1, a check failed) the global engine
+      // reports it, in TLC order on one rank
+      const int pr = W == 1 ? producer_error(c, evk) : 0;
+      if (pr < 0) return -1;
+      if (pr == 0) {
+        c->tree_event = true;
+        return 0;
+      }
+    }
     return 1;
   }
   return 0;  // a component past the largest chunk
@@ -2314,6 +2696,18 @@ bool run_init(tlcg_ctx* c) {
   c->kernel_ms = c->expand_ms = 0;
   c->levels_redone = 0;
   const int world = c->opts.world;
+  if (c->seed_valid) {  // level 0 = the one seed state (producer_error), one rank
+    if (!ensure_store(c, 1)) return false;
+    if (!rebuild_fpset(c, c->d_slots ? c->log2 : 16, 0)) return false;
+    uint64_t w[2] = {0, 0}, par = NO_PARENT;
+    split_words(c->seed_state, w, c->words);
+    HIPCHK(hipMemcpy(dev_state(c, 0), w, 8 * (size_t)c->words, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dev_parent(c, 0), &par, 8, hipMemcpyHostToDevice));
+    if (!rebuild_fpset(c, c->log2, 1)) return false;  // (inserts it)
+    c->generated = 1;
+    c->level_base.push_back(1);
+    return true;
+  }
   u64 expect = world == 1 ? hm.n_init : hm.n_init / (u64)world + hm.n_init / (u64)(4 * world) + 4096;
   expect = std::min(expect, hm.n_init);
   if (!ensure_store(c, expect)) return false;
@@ -2596,6 +2990,27 @@ bool trace_ranks(tlcg_ctx* c, Transport& t, int first, std::string* err) {
   const Layout& L = c->hm.L;
   const int me = t.rank(), w = c->words;
   const u64 ordmask = (1ull << L.ord_bits) - 1, refmask = (1ull << 56) - 1;
+  // a trace the first rank already holds (the component tree's closed mode
+  // replays the error's component, which lies on that rank): handed to all
+  uint64_t held = me == first && c->xtrace_valid ? (uint64_t)c->xtrace_states.size() : 0;
+  if (!t.allreduce(&held, 1, RED_SUM, err)) return false;
+  if (held) {
+    std::vector<uint64_t> buf((size_t)held * 3, 0);  // state words, action + 2
+    if (me == first)
+      for (size_t i = 0; i < (size_t)held; ++i) {
+        split_words(c->xtrace_states[i], &buf[i * 3], 2);
+        buf[i * 3 + 2] = (uint64_t)(c->xtrace_acts[i] + 2);
+      }
+    if (!t.allreduce(buf.data(), (int)buf.size(), RED_SUM, err)) return false;
+    c->xtrace_states.assign((size_t)held, 0);
+    c->xtrace_acts.assign((size_t)held, 0);
+    for (size_t i = 0; i < (size_t)held; ++i) {
+      c->xtrace_states[i] = join_words(&buf[i * 3], 2);
+      c->xtrace_acts[i] = (int)buf[i * 3 + 2] - 2;
+    }
+    c->xtrace_valid = true;
+    return true;
+  }
   c->xtrace_valid = false;
   c->xtrace_states.clear();
   c->xtrace_acts.clear();
@@ -2815,6 +3230,13 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
   if (!c || !c->stream) return -1;
   free_tier(c);
   free_host_chunks(c);
+  if (c->tlc_switched) {  // (the last run took TLC order for a tree error)
+    c->opts.tlc_order = 0;
+    c->tlc_switched = false;
+  }
+  c->tree_event = false;
+  c->ev_comp = ~0ull;
+  c->stop_cached = false;
   c->tree_codes = false;
   c->xtrace_valid = false;
   c->kernel_ms = c->expand_ms = 0;
@@ -2832,6 +3254,12 @@ int tlcg_init(tlcg_ctx* c, tlcg_stats* st) {
       c->inited = true;
       fill_stats(c, st);
       return 0;
+    }
+    // an error to report, on one rank: the global engine runs in TLC order,
+    // so its trace and TLC's stop statistics need no second run
+    if (c->tree_event && c->opts.world == 1 && !c->opts.tlc_order) {
+      c->opts.tlc_order = 1;
+      c->tlc_switched = true;
     }
   }
   if (c->opts.engine != TLCG_ENGINE_GLOBAL && c->opts.engine != TLCG_ENGINE_TREE && component_applicable(c)) {
@@ -3059,6 +3487,82 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
 
 }  // extern "C"
 
+namespace {
+
+// per-level sizes and generated counts of the on-chip engine's run over
+// initial states [0, hi) alone, in a context of its own (this one's store,
+// traces and counts stay as they are)
+bool prefix_counts(tlcg_ctx* c, u64 hi, std::vector<u64>* pl, std::vector<u64>* pg) {
+  tlcg_opts o = c->opts;
+  o.world = 1;
+  o.rank = 0;
+  o.engine = c->engine;
+  o.outdegree = 0;
+  o.tlc_order = 0;
+  o.state_capacity = 0;
+  o.log2_fpset_slots = 0;
+  tlcg_model m = c->model;
+  tlcg_ctx* t = nullptr;
+  if (tlcg_create(&m, &o, &t) != 0) {
+    c->err = std::string("TLC stop statistics: ") + (t ? t->err : "tlcg_create failed");
+    tlcg_destroy(t);
+    return false;
+  }
+  t->range_hi = hi;
+  t->comp_mult = c->comp_mult;  // (the tuned slot hashes: same code graph)
+  t->tree_mult = c->tree_mult;
+  t->tree_disp_mult = c->tree_disp_mult;
+  std::copy(c->tree_disp, c->tree_disp + TREE_DISP, t->tree_disp);
+  tlcg_stats st;
+  const bool ok = tlcg_init(t, &st) == 0 && t->engine == c->engine;
+  if (ok) {
+    *pl = t->comp_levels;
+    *pg = t->comp_level_gen;
+  } else {
+    c->err = "TLC stop statistics: the prefix run failed: " + t->err;
+  }
+  tlcg_destroy(t);
+  return ok;
+}
+
+// TLC's stop statistics of an on-chip engine's error on a closed partition
+// (replay_component): TLC's queue holds each level in component order, so
+// at its stop TLC has generated and found everything of levels before the
+// stopping state's, the components before the error's on the stopping
+// level (a prefix run: initial states [0, comp)), and the error component's
+// own share (its replay)
+int onchip_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, uint64_t* left_on_queue) {
+  const int E = c->ev_level;
+  const u64 comp = c->ev_comp;
+  if (E == 0) {  // an initial state: Init enumeration index comp, nothing dequeued yet
+    *generated = *distinct = *left_on_queue = comp + 1;
+    return 0;
+  }
+  CompReplay rp;
+  if (!replay_component(c, comp, &rp) || rp.level != E) {
+    c->err = "internal: the error's component replay disagrees with the engine";
+    return -10;
+  }
+  std::vector<u64> pl, pg;
+  if (comp > 0 && !prefix_counts(c, comp, &pl, &pg)) return -10;
+  auto at = [](const std::vector<u64>& v, int i) -> u64 { return i >= 0 && (size_t)i < v.size() ? v[(size_t)i] : 0; };
+  u64 gen = c->comp_init, dist = 0, before = 0;
+  for (int l = 0; l < E - 1; ++l) {
+    gen += at(c->comp_level_gen, l);
+    before += at(c->comp_levels, l);
+  }
+  for (int l = 0; l <= E - 1; ++l) dist += at(c->comp_levels, l);
+  gen += at(pg, E - 1) + rp.outdeg_before + rp.partial;
+  dist += at(pl, E) + rp.found_next;
+  const u64 pos = before + at(pl, E - 1) + rp.p_index;  // the stopping state's place in TLC's queue
+  *generated = gen;
+  *distinct = dist;
+  *left_on_queue = dist - (pos + 1);
+  return 0;
+}
+
+}  // namespace
+
 // TLC's statistics at the moment a one-worker run stops on the error this
 // context found (tlcgpu.h).  TLC's Worker dequeues states in FIFO order and,
 // per state, runs the Next disjuncts in order: each action's successors are
@@ -3076,8 +3580,18 @@ int tlcg_trace(tlcg_ctx* c, uint64_t* states, int32_t* actions, int32_t cap, int
 int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, uint64_t* left_on_queue) {
   const DeviceGuard dg(c);
   if (!c) return -1;
+  if (c->stop_cached && c->status >= TLCG_VIOLATION) {  // (worked out with the run: producer_error)
+    *generated = c->stop_g;
+    *distinct = c->stop_d;
+    *left_on_queue = c->stop_q;
+    return 0;
+  }
+  if (c->status >= TLCG_VIOLATION && c->opts.world == 1 && c->engine != TLCG_ENGINE_GLOBAL && !c->hm.L.producer &&
+      c->ev_comp != ~0ull)
+    return onchip_stop_stats(c, generated, distinct, left_on_queue);
   if (c->status < TLCG_VIOLATION || !c->opts.tlc_order || c->opts.world != 1 || c->engine != TLCG_ENGINE_GLOBAL) {
-    c->err = "TLC stop statistics need a global-engine run in TLC order (world 1) that stopped on an error";
+    c->err = "TLC stop statistics need a global-engine run in TLC order, or an on-chip engine's run of a closed "
+             "partition (world 1), that stopped on an error";
     return -2;
   }
   const Layout& L = c->hm.L;

@@ -145,6 +145,8 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   __syncthreads();
   unsigned flags = 0;
   uint32_t maxn = 0;
+  u64 evk = ~0ull;  // this lane's least error key (tree_event_key)
+  u64 subtree = 0;  // Producer modelled: the group's component's first message (its subtree), nkv for the root
   // a group's current component and its BFS state (uniform inside the group)
   u64 ci = (u64)blockIdx.x * G + (u64)g;
   const u64 cstep = (u64)gridDim.x * G;
@@ -229,12 +231,13 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         else st[pos] = code_word<W>(L, kc, msgs, key);
 #endif
 #ifndef TLCG_TREE_NO_INV  // (experiment only: what the invariants cost)
-        if (!TLCG_TREE_INV_AT_EXPAND && check_invariants_cb<W>(L, kc, key) >= 0) flags |= TREE_EVENT;  // the global engine reports it
+        if (!TLCG_TREE_INV_AT_EXPAND && check_invariants_cb<W>(L, kc, key) >= 0)
+          evk = min(evk, tree_event_key(dd, a.comp0 + ci));  // (the host replays the component)
 #endif
       } else {
         st[pos] = msgs | ((u64)key << mb);
         dp[pos] = (uint8_t)dd;  // (read by the next layer)
-        if (!TLCG_TREE_INV_AT_EXPAND_OPEN && check_invariants_k(L, cm, key) >= 0) flags |= TREE_EVENT;
+        if (!TLCG_TREE_INV_AT_EXPAND_OPEN && check_invariants_k(L, cm, key) >= 0) evk = min(evk, tree_event_key(dd, subtree));
       }
     }
     n = n + cnt > CAP ? CAP : n + cnt;
@@ -265,6 +268,11 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         pdep = a.layer ? a.par_dep + pc * CAP : nullptr;
         pgb = a.par_gbase + pc * CAP;
         const u64 w0 = a.layer == 0 ? init_state(L, 0) : producer_succ(L, pst[0], a.layer - 1, j);
+        {  // the subtree: the component's first message (Producer appends, compaction.tla:83-87)
+          u64 per = 1;
+          for (int l = 1; l < a.layer; ++l) per *= (u64)L.nkv;
+          subtree = a.layer == 0 ? (u64)L.nkv : (a.comp_base + ci) / per;
+        }
         msgs = (W)(w0 & L.msgs_mask);
         cm = comp_msgs_init(L, w0);        // everything that reads only `messages`
         nprod = cm.len < L.N ? L.nkv : 0;  // Producer's successors (into the children)
@@ -357,20 +365,23 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       bool crash;
       if constexpr (CLOSED) {
 #ifndef TLCG_TREE_NO_INV
-        if (TLCG_TREE_INV_AT_EXPAND && ok && check_invariants_cb<W>(L, kc, k) >= 0) flags |= TREE_EVENT;
+        if (TLCG_TREE_INV_AT_EXPAND && ok && check_invariants_cb<W>(L, kc, k) >= 0)
+          evk = min(evk, tree_event_key(d, a.comp0 + ci));
 #endif
         r = ok ? compactor_step_cb(L, kc, k, &t, &act) : 0;
         crash = ok && crash_step_c(L, k, &t2);
         nsucc = (r == 1) + (int)crash + selfloop_count_c(L, kc, k);
       } else {
-        if (TLCG_TREE_INV_AT_EXPAND_OPEN && ok && check_invariants_k(L, cm, k) >= 0) flags |= TREE_EVENT;
+        if (TLCG_TREE_INV_AT_EXPAND_OPEN && ok && check_invariants_k(L, cm, k) >= 0) evk = min(evk, tree_event_key(d, subtree));
         r = ok ? compactor_step_k(L, cm, (u64)msgs, k, k_phase(L, k), &t, &act) : 0;
         crash = ok && crash_step_k(L, k, &t2);
         nsucc = nprod + (r == 1) + (int)crash + selfloop_count_k(L, cm, k);
       }
       if (ok && !roleb) {
         gen += (unsigned)nsucc;
-        if (r == 2 || (nsucc == 0 && L.check_deadlock)) flags |= TREE_EVENT;
+        if (r == 2 || (nsucc == 0 && L.check_deadlock)) {
+          evk = min(evk, tree_event_key(d + 1, CLOSED ? a.comp0 + ci : subtree));
+        }
       }
       const u64 pref = (gb + (u64)i) << L.ord_bits;
       // (one call for the whole wave: the insert ballots across the lanes)
@@ -406,9 +417,12 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   const unsigned fo = __ballot(flags & TREE_OVERFLOW) ? TREE_OVERFLOW : 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) maxn = max(maxn, (uint32_t)__shfl_xor(maxn, off));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) evk = min(evk, (u64)__shfl_xor((unsigned long long)evk, off));
   if (lane == 0) {
     if (fl | fo) atomicOr(a.flags, fl | fo);
     atomicMax(a.max_n, maxn);
+    if (evk != ~0ull) atomicMin(a.event, (unsigned long long)evk);
   }
   __syncthreads();
   const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy

@@ -376,8 +376,10 @@ int main(int argc, char** argv) {
     tlcg_stats tst = st;
     bool own = false, use_node_trace = false;
     // (after -gpus N: on one GPU).  The global engine in TLC order stores the
-    // states in TLC's FIFO order, which also gives TLC's statistics at the stop.
-    if (o.trace && (!o.tlc_order || !ctx || st.engine != TLCG_ENGINE_GLOBAL)) {
+    // states in TLC's FIFO order, which also gives TLC's statistics at the stop;
+    // no re-run when the first run's trace and stop statistics already are
+    // TLC's (st.tlc_exact: the component engine's error on one GPU, a TLC-order run)
+    if (o.trace && !(ctx && st.tlc_exact) && (!o.tlc_order || !ctx || st.engine != TLCG_ENGINE_GLOBAL)) {
       tlcg_opts to = opts;
       to.tlc_order = 1;
       to.engine = TLCG_ENGINE_GLOBAL;

@@ -56,7 +56,7 @@ class tlcg_stats(C.Structure):
                 ("event_gidx", C.c_uint64), ("fp_collision_optimistic", C.c_double), ("kernel_ms", C.c_double),
                 ("expand_ms", C.c_double), ("levels_redone", C.c_uint64), ("engine", C.c_uint64),
                 ("jit_used", C.c_uint64), ("host_states", C.c_uint64), ("fpset_host_states", C.c_uint64),
-                ("transport", C.c_uint64)]
+                ("transport", C.c_uint64), ("tlc_exact", C.c_uint64)]
 
 
 class tlcg_liveness(C.Structure):
@@ -404,6 +404,7 @@ class Result:
     fpset_host_states: int = 0
     trace: List[Tuple[str, int]] = field(default_factory=list)
     transport: str = ""  # multi-rank runs: "local" (threads, device copies) or "rccl"
+    tlc_exact: bool = False  # an error whose trace and tlc_stop_stats() are TLC -workers 1's (tlcg_stats.tlc_exact)
 
 
 class Checker:
@@ -526,7 +527,7 @@ class Checker:
                    collision_optimistic=s.fp_collision_optimistic, kernel_ms=s.kernel_ms,
                    expand_ms=s.expand_ms, levels_redone=s.levels_redone,
                    engine={v: k for k, v in ENGINES.items()}.get(s.engine, "?"), host_states=s.host_states,
-                   fpset_host_states=s.fpset_host_states)
+                   fpset_host_states=s.fpset_host_states, tlc_exact=bool(s.tlc_exact))
         if s.invariant >= 0:
             r.invariant = self.model.invariants[s.invariant]
         if s.action >= 0:

@@ -37,7 +37,7 @@ def test_python_binding_covers_the_header():
 
 
 def test_abi_version():
-    assert tlcgpu.load_library().tlcg_abi_version() == 3
+    assert tlcgpu.load_library().tlcg_abi_version() == 4
 
 
 def test_struct_layout_matches_c(tmp_path):

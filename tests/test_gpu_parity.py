@@ -34,7 +34,7 @@ def check_against_golden(case, r, tlc_order):
     assert len(r.trace) == len(want_trace)
     if want["result"] == "invariant":
         assert r.invariant == want["invariant"]
-    if tlc_order or r.engine == "component":  # both reproduce TLC's -workers 1 trace
+    if tlc_order or r.engine == "component" or r.tlc_exact:  # each reproduces TLC's -workers 1 trace
         assert [a for a, _ in r.trace] == [t["action"] for t in want_trace]
         assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want_trace]
     else:
@@ -114,16 +114,50 @@ def test_outdegree_histogram(case, mode):
 
 
 def test_tlc_stop_statistics_need_tlc_order():
-    """Outside TLC order the store is not in TLC's FIFO order: refused."""
+    """The global engine outside TLC order: its store is not in TLC's FIFO
+    order, so its stop statistics are refused (the on-chip engines give them,
+    test_tlc_stop_statistics_without_a_rerun)."""
     m = model_of(GOLDEN["V_leak"]["constants"])
-    for kw in (dict(engine="global"), dict(engine="component")):
-        ck = tlcgpu.Checker(m, **kw)
-        try:
-            assert ck.run().status == "invariant"
-            with pytest.raises(RuntimeError):
-                ck.tlc_stop_stats()
-        finally:
-            ck.close()
+    ck = tlcgpu.Checker(m, engine="global")
+    try:
+        r = ck.run()
+        assert r.status == "invariant" and not r.tlc_exact
+        with pytest.raises(RuntimeError):
+            ck.tlc_stop_stats()
+    finally:
+        ck.close()
+
+
+@pytest.mark.parametrize("case", ERROR_CASES)
+def test_tlc_stop_statistics_without_a_rerun(case):
+    """the default engine reports TLC's first error itself.
+    Closed partitions: the component engine (TLC-order lanes) or the component
+    tree's closed mode (the error's component replayed in TLC's order on the
+    host) -- trace and TLC's stop counters with no global-engine run (the
+    components before the error's counted by a prefix run of the same
+    engine).  Producer modelled: the tree's error switches the one-rank run to
+    the global engine in TLC order, so its trace and counters need no second
+    run either."""
+    m = model_of(GOLDEN[case]["constants"])
+    want = GOLDEN[case]["result"]
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run()
+        assert r.status == want["result"]
+        if r.engine == "global" and not m.model_producer:
+            pytest.skip("no on-chip engine takes this model")
+        assert r.tlc_exact, (case, r.engine)
+        if m.model_producer:
+            assert r.engine == "global"
+        assert [a for a, _ in r.trace] == [t["action"] for t in want["trace"]], (case, r.engine)
+        assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+        assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"]), (case, r.engine)
+        # the same context checks again
+        r2 = ck.run()
+        assert (r2.status, r2.generated, r2.distinct, r2.engine) == (r.status, r.generated, r.distinct, r.engine)
+    finally:
+        ck.close()
 
 
 def component_key_fits(c):

@@ -89,10 +89,20 @@ def test_tree_parent_log_walks_to_init(case):
 def test_tree_error_falls_back_to_global(case):
     m = model_of(GOLDEN[case]["constants"])
     want = GOLDEN[case]["result"]
-    r = tlcgpu.run(m)  # auto: the tree finds the error, the global engine reports it
-    assert r.engine == "global"
-    assert r.status == want["result"] and r.depth == want["depth"]
-    assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+    ck = tlcgpu.Checker(m)  # auto: the tree finds the error, the global engine reports it in TLC order
+    try:
+        r = ck.run()
+        assert r.engine == "global" and r.tlc_exact
+        assert r.status == want["result"] and r.depth == want["depth"]
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+        if "trace" in want:
+            assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
+            assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"])
+        # the next check on the same context runs the tree again (fast order)
+        r2 = ck.run()
+        assert (r2.status, r2.generated, r2.distinct) == (r.status, r.generated, r.distinct)
+    finally:
+        ck.close()
 
 
 def test_p8_on_the_tree():

@@ -65,10 +65,12 @@ def test_user_invariant_check(case, order):
 
 @pytest.mark.parametrize("case", sorted(GOLD))
 def test_user_invariant_on_chip(case):
-    """the default engine: the component engine without a Producer (its lanes
-    keep TLC's order, so a violation's trace is TLC's -workers 1 trace), the
-    component tree with one (an error there is reported by the global engine's
-    re-run); the user invariants evaluated inside the specialized kernels"""
+    """the default engine with the user invariants inside its specialized
+    kernels: the component engine without a Producer (its lanes keep TLC's
+    order), the component tree's closed mode past a lane's 255 states (its
+    error replayed in TLC's order on the host), the component tree with a
+    Producer (its error reported by the global engine in TLC order); every
+    error's trace and TLC's stop counters are TLC's, with no second run"""
     m = model(case)
     want = GOLD[case]["result"]
     # (C = 5, K = 2: 302 states per component, past a lane's 255: the tree's closed mode)
@@ -82,16 +84,14 @@ def test_user_invariant_on_chip(case):
                                                                  want["levels"])
         ck.close()
         return
-    assert r.engine == ("global" if on_chip == "tree" else "component")
+    assert r.engine == ("global" if m.model_producer else on_chip) and r.tlc_exact
     assert r.depth == want["depth"]
     assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
     if want["result"] in ("invariant", "invariant_error"):
         assert r.invariant == want["invariant"]
-    if on_chip == "component":
-        assert [a for a, _ in r.trace] == [t["action"] for t in want["trace"]]
-        assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
-    else:
-        check_path(m, r, want)
+    assert [a for a, _ in r.trace] == [t["action"] for t in want["trace"]]
+    assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
+    assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"])
     ck.close()
 
 
@@ -99,20 +99,23 @@ def test_user_invariant_on_chip(case):
                                   "U_C5_ContextBound"])
 def test_user_invariant_tree_closed_mode(case):
     """the component tree's closed mode (components past a lane of the
-    component engine) with the user invariants in its kernel: counts of an
-    error-free check; an error is reported by the global engine's re-run"""
+    component engine) with the user invariants in its kernel; an error is
+    replayed in TLC's order on the host (trace, TLC's stop counters)"""
     m = model(case)
     want = GOLD[case]["result"]
-    r = tlcgpu.run(m, engine="tree")
+    ck = tlcgpu.Checker(m, engine="tree")
+    r = ck.run()
     assert r.status == want["result"], (case, r.status)
+    assert r.engine == "tree"
     if want["result"] == "ok":
-        assert r.engine == "tree"
         assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
                                                                  want["levels"])
     else:
-        assert r.engine == "global" and r.depth == want["depth"]
+        assert r.tlc_exact and r.depth == want["depth"]
         assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
-        check_path(m, r, want)
+        assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
+        assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"])
+    ck.close()
 
 
 @pytest.mark.parametrize("world", [2, 3])
