@@ -41,6 +41,9 @@ CONFIGS = {
     "g9uall": dict(keys=15, distinct=1_040_187_392, generated=1_392_508_928, depth=20,
                    user=("PhaseKnown", "LatestIsLast", "LedgerSorted", "KeysKnown", "MessageRec", "HeadFirst")),
 }
+# (and one config per user invariant alone: g9u_PhaseKnown, ...)
+for _n in ("PhaseKnown", "LatestIsLast", "LedgerSorted", "KeysKnown", "MessageRec", "HeadFirst"):
+    CONFIGS["g9u_" + _n] = dict(CONFIGS["g9"], user=_n)
 # user invariants the g9u* configs add to compaction.tla (definitions by name;
 # KeySet, ValueSet and NullKey are the module's own, restated for the library)
 USER_DEFS = {

@@ -79,13 +79,17 @@ __device__ __forceinline__ unsigned ovf_of(int r) { return r == -2 ? (unsigned)O
 template <typename W>
 __global__ __launch_bounds__(BLOCK) void k_user_check(Layout L, const UserProg* __restrict__ P,
                                                       const W* __restrict__ states, const u64* __restrict__ parents,
-                                                      u64 n, int level0, unsigned long long* ev) {
+                                                      u64 n, int level0, unsigned long long* ev, u64 rank_tag, u64 g0) {
   const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
   const int c = check_invariants_all(L, *P, states[i]);
   if (c < 0) return;
-  // (level 0: the Init number, which is the store position on one rank only)
-  const u64 dkey = level0 ? init_index(L, states[i]) : (parents[i] & ((1ull << 56) - 1));
+  // (level 0: the Init number, which is the store position on one rank only;
+  // a state absorbed from another rank, whose parent lives there: its own
+  // store index, tagged with bit 50, resolve_event)
+  const u64 pr = parents[i];
+  const u64 dkey = level0 ? init_index(L, states[i])
+                 : (pr & ~((1ull << 56) - 1)) != rank_tag ? (1ull << 50) | (g0 + i) : (pr & ((1ull << 56) - 1));
   atomicMin(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
 }
 
@@ -1750,6 +1754,16 @@ bool resolve_event(tlcg_ctx* c, u64 ev, int level) {
     c->ev_action = TLCG_ACT_INIT;
     return true;
   }
+  if (((dkey >> 50) & 3) == 1) {  // a state absorbed from another rank (k_user_check): its store index
+    u128 s = 0;
+    u64 p = 0;
+    if (!state_at(c, dkey & ((1ull << 50) - 1), &s, &p)) return false;
+    c->ev_state = s;
+    c->ev_parent_ref = p;
+    c->ev_parent_gidx = NO_PARENT;
+    c->ev_action = action_of_ordinal(L, (int)(p & ((1ull << L.ord_bits) - 1)));
+    return true;
+  }
   if ((dkey >> 51) & 1) {  // a state absorbed from another rank: inbox position
     const u64 i = dkey & ((1ull << 51) - 1);
     u64 rec[2];
@@ -2665,10 +2679,11 @@ u64 user_check_level(tlcg_ctx* c, u64 g0, u64 n, bool level0) {
   const unsigned g = grid_for(n, BLOCK, 0x7fffffffu);
   if (c->words == 1)
     k_user_check<u64><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, dev_state(c, g0), dev_parent(c, g0), n,
-                                                   level0 ? 1 : 0, c->d_uev);
+                                                   level0 ? 1 : 0, c->d_uev, (u64)c->opts.rank << 56, g0);
   else
     k_user_check<u128><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, (const u128*)dev_state(c, g0),
-                                                    dev_parent(c, g0), n, level0 ? 1 : 0, c->d_uev);
+                                                    dev_parent(c, g0), n, level0 ? 1 : 0, c->d_uev,
+                                                    (u64)c->opts.rank << 56, g0);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(&h, c->d_uev, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess) {

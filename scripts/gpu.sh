@@ -12,6 +12,7 @@
 #   pmc:NAME:KERNEL:CASE          PMC groups of one check (scripts/pmc_kernel.sh CASE KERNEL NAME)
 #   probe:NAME:CASE,CASE,...      scripts/probe.py CASEs -> gpurun_out/probe_NAME.jsonl
 #   node:NAME:ARGS                scripts/node_bench.py ARGS -> gpurun_out/node_NAME.jsonl
+#   py:NAME:SCRIPT,ARGS           python SCRIPT ARGS -> gpurun_out/py_NAME.log
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -65,6 +66,12 @@ for step in "$@"; do
       timeout -k 10 600 python -u scripts/node_bench.py "${args[@]}" > "gpurun_out/node_$name.jsonl" 2>&1 \
         || { echo "node $name failed"; tail -20 "gpurun_out/node_$name.jsonl"; exit 1; }
       cut -c1-400 "gpurun_out/node_$name.jsonl" ;;
+    py)
+      name="${rest%%:*}"; a="${rest#*:}"
+      IFS=',' read -r -a args <<< "$a"
+      timeout -k 10 600 python -u "${args[@]}" > "gpurun_out/py_$name.log" 2>&1 \
+        || { echo "py $name failed"; tail -20 "gpurun_out/py_$name.log"; exit 1; }
+      cut -c1-400 "gpurun_out/py_$name.log" | tail -20 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -148,7 +148,7 @@ def test_tlc_stop_statistics_without_a_rerun(case):
             pytest.skip("no on-chip engine takes this model")
         assert r.tlc_exact, (case, r.engine)
         if m.model_producer:
-            assert r.engine == "global"
+            assert r.engine in ("tree", "global")
         assert [a for a, _ in r.trace] == [t["action"] for t in want["trace"]], (case, r.engine)
         assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
         assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])

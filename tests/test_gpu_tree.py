@@ -86,13 +86,13 @@ def test_tree_parent_log_walks_to_init(case):
 
 
 @pytest.mark.parametrize("case", ERR_CASES)
-def test_tree_error_falls_back_to_global(case):
+def test_tree_error_reported_without_a_global_run(case):
     m = model_of(GOLDEN[case]["constants"])
     want = GOLDEN[case]["result"]
-    ck = tlcgpu.Checker(m)  # auto: the tree finds the error, the global engine reports it in TLC order
+    ck = tlcgpu.Checker(m)  # auto: the tree finds the error and reports it (its subtree's TLC-order run)
     try:
         r = ck.run()
-        assert r.engine == "global" and r.tlc_exact
+        assert r.engine == "tree" and r.tlc_exact
         assert r.status == want["result"] and r.depth == want["depth"]
         assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
         if "trace" in want:
@@ -151,23 +151,32 @@ def tree_applies(m):
 @pytest.mark.parametrize("seed", range(60))
 def test_tree_random_producer_cfgs(seed):
     """Seeded random producer-modelled cfgs against the C oracle run live: the
-    tree's counts and every level when the check passes, and on an error the
-    global engine's verdict and depth (the tree hands the model over)."""
+    tree's counts and every level when the check passes; on an error the
+    verdict, the depth, the end-of-level counts, TLC's trace and TLC's stop
+    counters, reported by the tree (its erroring subtree run in TLC order) or
+    by the global engine in TLC order (an error of the root component or at
+    level 1, or a model the tree does not take)."""
     from conftest import run_oracle
     m = random_producer_model(seed)
     if tlcgpu.check_model(m) is not None:
         pytest.skip(f"constants refused: {tlcgpu.check_model(m)}")
     want = run_oracle(m)
-    r = tlcgpu.run(m)
+    ck = tlcgpu.Checker(m)
+    r = ck.run()
+    stop = ck.tlc_stop_stats() if r.status != "ok" else None
+    ck.close()
     assert r.status == want["result"], (seed, r.status, want["result"])
     assert r.depth == want["depth"], seed
     if want["result"] == "ok":
         assert (r.generated, r.distinct, r.levels) == (want["generated"], want["distinct"], want["levels"]), seed
         assert r.engine == ("tree" if tree_applies(m) else "global"), (seed, r.engine)
     else:
-        assert r.engine == "global", seed
+        assert r.engine in ("tree", "global") and r.tlc_exact, (seed, r.engine)
         if want["result"] in ("invariant", "invariant_error"):
             assert r.invariant == want["invariant"], seed
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"]), seed
+        assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]], seed
+        assert stop == (want["generated"], want["distinct"], want["left_on_queue"]), (seed, r.engine)
 
 
 @pytest.mark.parametrize("ranks", [2, 3, 8])

@@ -73,8 +73,8 @@ def test_user_invariant_on_chip(case):
     error's trace and TLC's stop counters are TLC's, with no second run"""
     m = model(case)
     want = GOLD[case]["result"]
-    # (C = 5, K = 2: 302 states per component, past a lane's 255: the tree's closed mode)
-    on_chip = "tree" if m.model_producer or case == "U_C5K2_MaxLedgerBound" else "component"
+    # (C = 5: the local key passes 32 bits, or 302 states per component at K = 2: the tree's closed mode)
+    on_chip = "tree" if m.model_producer or case.startswith("U_C5") else "component"
     ck = tlcgpu.Checker(m)
     r = ck.run()
     assert r.status == want["result"], (case, r.status)
@@ -84,7 +84,7 @@ def test_user_invariant_on_chip(case):
                                                                  want["levels"])
         ck.close()
         return
-    assert r.engine == ("global" if m.model_producer else on_chip) and r.tlc_exact
+    assert r.engine == on_chip and r.tlc_exact
     assert r.depth == want["depth"]
     assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
     if want["result"] in ("invariant", "invariant_error"):
