@@ -435,7 +435,8 @@ int tlcg_checkpoint(tlcg_ctx* c, const char* path);
 int tlcg_recover(tlcg_ctx* c, const char* path, tlcg_stats* st);
 
 /* Diagnostic: compile the kernels specialized for these constants (hipRTC)
- * for `arch` without a device; returns the code-object size or <0 (err). */
+ * for `arch` without a device (with user invariants: also the global engine's
+ * user-check module); returns the code-object bytes or <0 (err). */
 int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t cap);
 
 /* HIP stream (hipStream_t) the context launches on, for event timing. */

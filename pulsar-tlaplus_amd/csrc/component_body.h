@@ -94,9 +94,15 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 // FPSet probes, so the VALU work overlaps the probes' LDS round trips (a
 // successor found seen evaluated them in vain: 1.34 evaluations per new
 // state instead of 1).  G9 4.84 -> 4.62 ms, M8 0.575 -> 0.546 ms
-// (profiles/r03_comp_spec_inv_ab.jsonl).  0: evaluated on insert, for A/B
+// (profiles/r03_comp_spec_inv_ab.jsonl).  0: evaluated on insert -- the
+// default with user invariants, whose VALU work is more than the probes hide
+// (G9 + LatestIsLast 6.46 -> 5.42 ms, profiles/r04_probe_uinv.jsonl)
 #ifndef TLCG_SPEC_INV
+#ifdef TLCG_USER_INV
+#define TLCG_SPEC_INV 0
+#else
 #define TLCG_SPEC_INV 1
+#endif
 #endif
 // component codes: the queue entry behind the second successor's first FPSet
 // slot read before the first successor's probe (A/B)

@@ -34,7 +34,9 @@ std::string layout_literal(const Layout& L) {
   return o.str();
 }
 
-std::string program_source(const Layout& L, const std::string& user) {
+// check_only: the user-invariant check kernel alone (tlcg_user_check, the
+// global engine's; compiles in a fraction of the whole module's time)
+std::string program_source(const Layout& L, const std::string& user, bool check_only = false) {
   std::string s = "typedef unsigned char uint8_t; typedef unsigned short uint16_t; typedef unsigned int uint32_t; typedef int int32_t;\n"
                   "typedef unsigned long uint64_t; typedef long int64_t;\n";
   // user invariants: the headers' check functions call tlcg_user_eval (model.h)
@@ -55,6 +57,13 @@ std::string program_source(const Layout& L, const std::string& user) {
   s += kJitSource;
   s += "\n" + layout_literal(L);
   s += user;
+  // the layout's word: u64, or u128 past 63 bits
+  const std::string w = L.bits <= 63 ? "tlcg::u64" : "tlcg::u128";
+  if (check_only) {
+    s += "extern \"C\" __global__ __launch_bounds__(256) void tlcg_user_check(tlcg::UserCheckArgs a) "
+         "{ tlcg::user_check_body<" + w + ">(a, kL); }\n";
+    return s;
+  }
   for (int K : {32, 64, 128, 255})
     for (const char* od : {"false", "true"})
       for (const char* code : {"false", "true"}) {
@@ -69,8 +78,7 @@ std::string program_source(const Layout& L, const std::string& user) {
        "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_1024(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<1024, 2048, 1>(a, kL); }\n";
-  // the closed mode on this layout's word (u64, or u128 past 63 bits)
-  const std::string w = L.bits <= 63 ? "tlcg::u64" : "tlcg::u128";
+  // (the closed mode on the layout's word)
   // (TLCG_TREEC_G: components per wavefront of the closed mode, a tuning
   // hook; the launch grid is the same, the kernel strides over the rest)
   s += "#ifndef TLCG_TREEC_G\n#define TLCG_TREEC_G 4\n#endif\n";
@@ -102,9 +110,11 @@ bool read_all(const std::string& p, std::vector<char>* out) {
 }  // namespace
 
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
-                 const std::string& user) {
-  const std::string src = program_source(L, user);
-  if (const char* dump = std::getenv("TLCG_JIT_DUMP")) {  // diagnostics: the generated source
+                 const std::string& user, bool check_only) {
+  const std::string src = program_source(L, user, check_only);
+  const char* dump_env = std::getenv("TLCG_JIT_DUMP");  // diagnostics: the generated source and code object
+  const std::string dump = dump_env ? std::string(dump_env) + (check_only ? ".check" : "") : "";
+  if (dump_env) {
     std::ofstream f(dump);
     f << src;
   }
@@ -136,14 +146,19 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
   code->resize(n);
   hiprtcGetCode(prog, code->data());
   hiprtcDestroyProgram(&prog);
-  if (const char* dump = std::getenv("TLCG_JIT_DUMP")) {
-    std::ofstream f(std::string(dump) + ".co", std::ios::binary);
+  if (dump_env) {
+    std::ofstream f(dump + ".co", std::ios::binary);
     f.write(code->data(), (std::streamsize)code->size());
   }
   return true;
 }
 
-bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user) {
+namespace {
+
+// the code object of program_source(L, user, check_only) for `device`: from the
+// cache, else compiled and cached; loaded into *module
+bool load_module(const Layout& L, int device, const std::string& user, bool check_only, hipModule_t* module,
+                 bool* cached, double* compile_s, std::string* err) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
     *err = "hipGetDeviceProperties failed";
@@ -151,18 +166,18 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
   }
   std::string arch = prop.gcnArchName;
   arch = arch.substr(0, arch.find(':'));
-  const std::string src = program_source(L, user);
+  const std::string src = program_source(L, user, check_only);
   char key[64];
   const char* jo = std::getenv("TLCG_JIT_OPTS");
   std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2" + (jo ? jo : "")));
   const std::string dir = cache_dir();
   const std::string path = dir + "/" + key + "-" + arch + ".co";
   std::vector<char> code;
-  out->cached = read_all(path, &code);
-  if (!out->cached) {
+  *cached = read_all(path, &code);
+  if (!*cached) {
     auto t0 = std::chrono::steady_clock::now();
-    if (!jit_compile(L, arch, &code, err, user)) return false;
-    out->compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!jit_compile(L, arch, &code, err, user, check_only)) return false;
+    *compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     mkdir(dir.c_str(), 0777);
     const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
     std::ofstream f(tmp, std::ios::binary);
@@ -171,10 +186,43 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
       std::rename(tmp.c_str(), path.c_str());
     }
   }
-  if (hipModuleLoadData(&out->module, code.data()) != hipSuccess) {
+  if (hipModuleLoadData(module, code.data()) != hipSuccess) {
     *err = "hipModuleLoadData failed for the specialized kernels";
     return false;
   }
+  return true;
+}
+
+}  // namespace
+
+bool jit_build_user_check(const Layout& L, int device, const std::string& user, JitUserCheck* out, std::string* err) {
+  double cs = 0;
+  bool cached = false;
+  if (!load_module(L, device, user, true, &out->module, &cached, &cs, err)) return false;
+  out->compile_s = cs;
+  if (hipModuleGetFunction(&out->fn, out->module, "tlcg_user_check") != hipSuccess) {
+    *err = "hipModuleGetFunction tlcg_user_check";
+    return false;
+  }
+  return true;
+}
+
+void jit_release_user_check(JitUserCheck* k) {
+  if (k && k->module) hipModuleUnload(k->module);
+  if (k) *k = JitUserCheck();
+}
+
+bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStream_t stream) {
+  if (!a.n) return true;
+  const uint64_t blocks = (a.n + 255) / 256;
+  if (blocks > 0x7fffffffull) return false;
+  UserCheckArgs copy = a;
+  void* args[] = {&copy};
+  return hipModuleLaunchKernel(k.fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, stream, args, nullptr) == hipSuccess;
+}
+
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user) {
+  if (!load_module(L, device, user, false, &out->module, &out->cached, &out->compile_s, err)) return false;
   const char* names[4] = {"32", "64", "128", "255"};
   for (int i = 0; i < 4; ++i)
     for (int od = 0; od < 2; ++od) {

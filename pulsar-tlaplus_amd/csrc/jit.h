@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "component.h"
+#include "kernels.h"
 #include "tree.h"
 
 namespace tlcg {
@@ -30,10 +31,23 @@ struct JitKernels {
 // which the kernels then evaluate in the cfg's order with the spec's own.
 bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user = "");
 // compile only (no device needed): the code object for `arch`
+// (check_only: the user-check kernel alone, jit_build_user_check)
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
-                 const std::string& user = "");
+                 const std::string& user = "", bool check_only = false);
 void jit_release(JitKernels* k);
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream);
+// the global engine's user-invariant check (kernels.h user_check_body) as
+// device code: a module of its own, so a global-engine check does not wait
+// for the on-chip engines' kernels to compile
+struct JitUserCheck {
+  hipModule_t module = nullptr;
+  hipFunction_t fn = nullptr;
+  double compile_s = 0;
+};
+bool jit_build_user_check(const Layout& L, int device, const std::string& user, JitUserCheck* out, std::string* err);
+void jit_release_user_check(JitUserCheck* k);
+bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStream_t stream);
+
 // the specialized tree kernel for cap 384 / 640 (4 groups) or 1024 / 2048 (1 group); false when not built or on a
 // launch error
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream);

@@ -174,4 +174,47 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
   return v;
 }
 
+// ---- the global engine's check of a new level [g0, g0 + n) when the cfg has
+// user invariants (Layout.defer_inv: the expand kernels check none).  Every
+// invariant in cfg order on each state; the event key is the state's
+// first-discovery key -- its parent reference without the rank, its Init
+// index on level 0, or (bit 50) its own store index when its parent lives on
+// another rank (tlcgpu.hip resolve_event).  The precompiled k_user_check
+// interprets the user program (user_inv.h); the hipRTC build (jit.cpp
+// tlcg_user_check) runs it as device code.
+struct UserCheckArgs {
+  const void* states;
+  const u64* parents;
+  u64 n;
+  int level0;
+  unsigned long long* ev;
+  u64 rank_tag;  // this rank << 56
+  u64 g0;
+};
+
+template <typename W>
+TLCG_HD u64 user_check_dkey(const Layout& L, const UserCheckArgs& a, u64 i, W s) {
+  const u64 pr = a.parents[i];
+  return a.level0 ? init_index(L, s)
+       : (pr & ~((1ull << 56) - 1)) != a.rank_tag ? (1ull << 50) | (a.g0 + i) : (pr & ((1ull << 56) - 1));
+}
+
+#ifdef TLCG_USER_INV
+template <typename W>
+__device__ __forceinline__ void user_check_body(const UserCheckArgs& a, const Layout& L) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const W s = ((const W*)a.states)[i];
+  int c = -1;
+  for (int q = 0; q < L.n_inv && c < 0; ++q) {
+    const int kind = L.inv[q];
+    const int r = kind >= INV_USER ? tlcg_user_eval(kind - INV_USER, UVWord<W>{L, s}) : eval_invariant(L, kind, s);
+    if (r != EV_TRUE) c = (q << 1) | (r == EV_ERROR ? 1 : 0);
+  }
+  if (c < 0) return;
+  atomicMin(a.ev, (unsigned long long)make_event(user_check_dkey(L, a, i, s), (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
+                                                 c >> 1));
+}
+#endif
+
 }  // namespace tlcg

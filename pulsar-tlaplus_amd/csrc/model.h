@@ -214,6 +214,21 @@ TLCG_HD int highbit64(u64 x) {  // index of the highest set bit, x != 0
   return 63 - __builtin_clzll(x);
 #endif
 }
+// user_inv.h U_NTH: the 1-based position of the j-th set bit of m among bits
+// 1..63 (bit 64 excluded), 0 when j < 1 or m has fewer set bits
+TLCG_HD long long ui_nth(u64 m, long long j) {
+  // (a scan to the j-th set bit: in the specialized kernels this keeps G9 +
+  // LatestIsLast at 67 VGPRs, where clearing the lowest bits and a find-first
+  // takes 90 -- 5.42 vs 7.73 ms, profiles/r04_probe_uinv5.jsonl)
+  const long long want = j;
+  long long pos = 0;
+  for (int p = 1; p <= 63 && m; ++p, m >>= 1)
+    if ((m & 1) && --j == 0) {
+      pos = p;
+      break;
+    }
+  return j > 0 || want < 1 ? 0 : pos;
+}
 
 template <typename W>
 TLCG_HD int highbit(W x) {  // x != 0

@@ -76,21 +76,17 @@ __device__ __forceinline__ unsigned ovf_of(int r) { return r == -2 ? (unsigned)O
 // first-discovery key -- its parent reference without the rank, or its Init
 // index on level 0 -- as the expand kernels' (kernels.h make_event), so the
 // least event of a level is TLC's first error there in TLC-order mode.
+// (kernels.h user_check_body is the hipRTC kernel; this one interprets the
+// program, for TLCG_JIT=0 or a failed hipRTC build)
 template <typename W>
-__global__ __launch_bounds__(BLOCK) void k_user_check(Layout L, const UserProg* __restrict__ P,
-                                                      const W* __restrict__ states, const u64* __restrict__ parents,
-                                                      u64 n, int level0, unsigned long long* ev, u64 rank_tag, u64 g0) {
+__global__ __launch_bounds__(BLOCK) void k_user_check(Layout L, const UserProg* __restrict__ P, UserCheckArgs a) {
   const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
-  if (i >= n) return;
-  const int c = check_invariants_all(L, *P, states[i]);
+  if (i >= a.n) return;
+  const W s = ((const W*)a.states)[i];
+  const int c = check_invariants_all(L, *P, s);
   if (c < 0) return;
-  // (level 0: the Init number, which is the store position on one rank only;
-  // a state absorbed from another rank, whose parent lives there: its own
-  // store index, tagged with bit 50, resolve_event)
-  const u64 pr = parents[i];
-  const u64 dkey = level0 ? init_index(L, states[i])
-                 : (pr & ~((1ull << 56) - 1)) != rank_tag ? (1ull << 50) | (g0 + i) : (pr & ((1ull << 56) - 1));
-  atomicMin(ev, (unsigned long long)make_event(dkey, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
+  atomicMin(a.ev, (unsigned long long)make_event(user_check_dkey(L, a, i, s), (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
+                                                 c >> 1));
 }
 
 // ---- Init (compaction.tla:188-202), world == 1: initial state idx goes to
@@ -895,6 +891,11 @@ struct tlcg_ctx {
   u64 ovf_cap = 0;
   // layout-specialized kernels (jit.cpp): 0 untried, 1 built, -1 failed (precompiled ones used)
   JitKernels jit;
+  tlcg_ctx* sub = nullptr;  // the Producer tree's subtree runs (producer_error), kept for the next error
+  u64 sub_cap = 0;          // its state capacity
+  JitUserCheck ujit;  // the global engine's user-invariant check as device code
+  int ujit_state = 0; // 0 not built, 1 built, 2 borrowed from the context that made this one, -1 failed
+                      // (k_user_check interprets)
   int jit_state = 0;
   bool jit_used = false;
   bool comp_code = false;  // the component engine's first pass runs component codes
@@ -2271,6 +2272,8 @@ bool tree_closed_applicable(const tlcg_ctx* c) {
 // depth as a missing state), which checks the argument on the run itself;
 // the subtrees before the erroring one (rarely any) are run to level E the
 // same way.  Returns 1 reported, 0 the global engine must report it, -1 error.
+void ensure_user_check(tlcg_ctx* c);
+
 namespace {
 
 // the tree's depth histogram of subtree m (levels 0..maxd), from the depth bytes of its chunks
@@ -2295,36 +2298,64 @@ bool subtree_depths(tlcg_ctx* c, u64 m, int maxd, std::vector<u64>* hist) {
 
 // a TLC-order run of subtree m to level E (absolute; its level r is level r + 1):
 // the context, stopped on an error or after level E; nullptr on failure
+// (TLCG_TIMING=1: the phases' wall times on stderr)
+void phase_note(const char* what, double t0) {
+  static const bool on = [] {
+    const char* v = std::getenv("TLCG_TIMING");
+    return v && std::atoi(v) != 0;
+  }();
+  if (on) std::fprintf(stderr, "[tlcg] %s %.3f ms\n", what, wall_ms() - t0);
+}
+
 tlcg_ctx* subtree_run(tlcg_ctx* c, u64 m, int E) {
   const Layout& L = c->hm.L;
-  tlcg_opts o = c->opts;
-  o.world = 1;
-  o.rank = 0;
-  o.engine = TLCG_ENGINE_GLOBAL;
-  o.tlc_order = 1;
-  o.outdegree = 0;
-  o.state_capacity = 0;
-  o.log2_fpset_slots = 0;
-  o.fpset_spill = 0;
-  o.device_store_cap = 0;
-  tlcg_model md = c->model;
-  tlcg_ctx* t = nullptr;
-  if (tlcg_create(&md, &o, &t) != 0) {
-    tlcg_destroy(t);
-    return nullptr;
+  const double t0 = wall_ms();
+  // sized from the tree's depth histogram of the subtree (its levels 1..E
+  // are the run's; a larger run fails subtree_run_matches anyway), so the
+  // FPSet and the store never regrow
+  std::vector<u64> hist;
+  if (!subtree_depths(c, m, E, &hist)) return nullptr;
+  u64 n = 0;
+  for (size_t l = 1; l < hist.size(); ++l) n += hist[l];
+  if (c->sub && c->sub_cap < n + n / 8 + 4096) {  // (too small for this subtree: made again)
+    tlcg_destroy(c->sub);
+    c->sub = nullptr;
   }
+  if (!c->sub) {
+    tlcg_opts o = c->opts;
+    o.world = 1;
+    o.rank = 0;
+    o.engine = TLCG_ENGINE_GLOBAL;
+    o.tlc_order = 1;
+    o.outdegree = 0;
+    o.state_capacity = n + n / 4 + 4096;  // (headroom for the next error's subtree)
+    int log2 = 16;
+    while ((1ull << log2) < 2 * o.state_capacity && log2 < 40) ++log2;
+    o.log2_fpset_slots = log2;
+    o.fpset_spill = 0;
+    o.device_store_cap = 0;
+    tlcg_model md = c->model;
+    if (tlcg_create(&md, &o, &c->sub) != 0) {
+      tlcg_destroy(c->sub);
+      c->sub = nullptr;
+      return nullptr;
+    }
+    c->sub_cap = o.state_capacity;
+    ensure_user_check(c);  // (one module for every subtree run of this context)
+    if (c->ujit_state == 1) {
+      c->sub->ujit = c->ujit;
+      c->sub->ujit_state = 2;
+    }
+  }
+  tlcg_ctx* t = c->sub;
+  phase_note("subtree create", t0);
   t->seed_valid = true;
   t->seed_state = producer_succ<u64>(L, init_state<u64>(L, 0), 0, (int)m);
   tlcg_stats st;
-  if (tlcg_init(t, &st) != 0) {
-    tlcg_destroy(t);
-    return nullptr;
-  }
+  if (tlcg_init(t, &st) != 0) return nullptr;
   while (t->status == TLCG_RUNNING && (int)t->level_base.size() - 1 < E)
-    if (tlcg_step_level(t, &st) != 0) {
-      tlcg_destroy(t);
-      return nullptr;
-    }
+    if (tlcg_step_level(t, &st) != 0) return nullptr;
+  phase_note("subtree run", t0);
   return t;
 }
 
@@ -2361,9 +2392,9 @@ int producer_error(tlcg_ctx* c, u64 evk) {
       pre_l += lv(E - 1);
       pre_gen += E - 1 < ng ? lg[(size_t)E - 1] : 0;  // (lg[k]: generated by expanding relative level k - 1)
     }
-    tlcg_destroy(t);
     if (!good) return 0;
   }
+  const double t0 = wall_ms();
   tlcg_ctx* t = subtree_run(c, sub, E);
   if (!t) return 0;
   int res = 0;
@@ -2425,7 +2456,7 @@ int producer_error(tlcg_ctx* c, u64 evk) {
     c->expand_ms += t->expand_ms;
     res = 1;
   }
-  tlcg_destroy(t);
+  phase_note("subtree report", t0);
   return res;
 }
 
@@ -2670,20 +2701,36 @@ int run_tree(tlcg_ctx* c) {
   return 0;  // a component past the largest chunk
 }
 
+// the global engine's user-check module (jit.h JitUserCheck), built once per
+// context (hipRTC; cached on disk after the first build)
+void ensure_user_check(tlcg_ctx* c) {
+  if (c->ujit_state != 0 || !c->hm.user) return;
+  std::string e;
+  c->ujit_state = !jit_off() && jit_build_user_check(c->hm.L, c->opts.device, c->user_src, &c->ujit, &e) ? 1 : -1;
+  if (c->ujit_state < 0 && !jit_off()) c->jit_error = e;
+}
+
 // the least user-invariant event of the new level [g0, g0 + n) (NO_EVENT: none,
 // or no user invariants); ~0ull - 1 on a launch error
 u64 user_check_level(tlcg_ctx* c, u64 g0, u64 n, bool level0) {
   if (!c->hm.user || !n) return NO_EVENT;
   unsigned long long h = NO_EVENT;
   if (hipMemcpyAsync(c->d_uev, &h, sizeof h, hipMemcpyHostToDevice, c->stream) != hipSuccess) return ~0ull - 1;
-  const unsigned g = grid_for(n, BLOCK, 0x7fffffffu);
-  if (c->words == 1)
-    k_user_check<u64><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, dev_state(c, g0), dev_parent(c, g0), n,
-                                                   level0 ? 1 : 0, c->d_uev, (u64)c->opts.rank << 56, g0);
-  else
-    k_user_check<u128><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, (const u128*)dev_state(c, g0),
-                                                    dev_parent(c, g0), n, level0 ? 1 : 0, c->d_uev,
-                                                    (u64)c->opts.rank << 56, g0);
+  const UserCheckArgs a = {dev_state(c, g0), dev_parent(c, g0), n, level0 ? 1 : 0, c->d_uev,
+                           (u64)c->opts.rank << 56, g0};
+  ensure_user_check(c);
+  if (c->ujit_state >= 1) {
+    if (!jit_launch_user_check(c->ujit, a, c->stream)) {
+      c->err = "user-invariant check launch failed";
+      return ~0ull - 1;
+    }
+  } else {
+    const unsigned g = grid_for(n, BLOCK, 0x7fffffffu);
+    if (c->words == 1)
+      k_user_check<u64><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, a);
+    else
+      k_user_check<u128><<<g, BLOCK, 0, c->stream>>>(c->hm.L, c->d_prog, a);
+  }
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(&h, c->d_uev, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -3216,7 +3263,10 @@ void tlcg_destroy(tlcg_ctx* c) {
   hipFree(c->d_aux);
   hipFree(c->d_prog);
   hipFree(c->d_uev);
+  tlcg_destroy(c->sub);
+  c->sub = nullptr;
   jit_release(&c->jit);
+  if (c->ujit_state == 1) jit_release_user_check(&c->ujit);
   hipFree(c->d_comp);
   hipFree(c->d_crec);
   hipFree(c->d_tree_dep);
@@ -4003,8 +4053,14 @@ int tlcg_jit_selftest(const tlcg_model* m, const char* arch, char* err, int32_t 
     if (err && cap > 0) std::snprintf(err, (size_t)cap, "%s", e.c_str());
     return -2;
   }
+  // (user invariants: the global engine's check module too)
+  std::vector<char> check;
+  if (hm.user && !jit_compile(hm.L, arch ? arch : "gfx950", &check, &e, user_device_source(*hm.user), true)) {
+    if (err && cap > 0) std::snprintf(err, (size_t)cap, "user-check module: %s", e.c_str());
+    return -2;
+  }
   if (err && cap > 0) err[0] = 0;
-  return (int)code.size();
+  return (int)(code.size() + check.size());
 }
 
 // Let devices 0..n-1 read and write each other's memory (xGMI peer access),

@@ -31,6 +31,7 @@
 #include "user_inv.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -1889,7 +1890,41 @@ class Compiler {
   // evaluates every element of a set whose elements can fail (TLC builds the set first)
   void force(const NodeP& at, const Val& s) {
     if (!can_fail(s.node)) return;
+    if (s.node->k == Node::BIN && s.node->s == "..") {  // a range's elements cannot fail once its bounds are known
+      integer(s.node->c[0], s.env);
+      integer(s.node->c[1], s.env);
+      return;
+    }
+    const int n0 = P_->n_ins, nr = nreg_;
     iterate(at, s, [&](const Val&) {});
+    // a loop none of whose elements can fail is dropped: the set's own
+    // evaluation (its failures included) is repeated by the iteration that
+    // follows, and an empty loop only costs the check its time
+    if (!loop_can_fail(n0, P_->n_ins)) {
+      P_->n_ins = n0;
+      nreg_ = nr;
+    }
+  }
+  // whether the code [n0, n) holds a loop (a backward jump and its target)
+  // that can fail: an error-raising instruction inside it, or a jump from
+  // inside it to somewhere other than the loop or its exit
+  bool loop_can_fail(int n0, int n) const {
+    auto jump = [](uint8_t op) { return op == U_JMP || op == U_JZ || op == U_JNZ; };
+    auto raises = [](uint8_t op) {
+      return op == U_ERR || op == U_ADD || op == U_SUB || op == U_MUL || op == U_NEG || op == U_DIV ||
+             op == U_MOD || op == U_RET;
+    };
+    for (int j = n0; j < n; ++j) {
+      const UInsn& b = P_->ins[j];
+      if (!jump(b.op) || b.imm > j) continue;
+      if (b.imm < n0) return true;
+      for (int k = b.imm; k <= j; ++k) {
+        const UInsn& in = P_->ins[k];
+        if (raises(in.op)) return true;
+        if (jump(in.op) && (in.imm < b.imm || in.imm > j + 1)) return true;
+      }
+    }
+    return false;
   }
   static bool can_fail(const NodeP& n) {
     if (!n) return false;
@@ -2091,7 +2126,10 @@ std::string user_device_source(const UserProg& P) {
         if (back) o << "if (++loops > " << UI_MAXLOOP << ") return EV_ERROR; ";
         o << "goto L" << in.imm << "; }\n";
       };
-      auto ovf = [&]() { o << "  if (ui_overflows(" << a << ")) return EV_ERROR;\n"; };
+      const std::string B = b, C = c;
+      auto arith = [&](const std::string& e) {
+        o << "  { const long long t = " << e << "; if (ui_overflows(t)) return EV_ERROR; " << a << " = t; }\n";
+      };
       switch (in.op) {
         case U_LDI: o << "  " << a << " = " << in.imm << "LL;\n"; break;
         case U_MOV: o << "  " << a << " = " << b << ";\n"; break;
@@ -2121,17 +2159,17 @@ std::string user_device_source(const UserProg& P) {
             << "      if (" << table_expr(P.keyval, P.nk, "x") << " == " << b << ") best = i;\n"
             << "    }\n    " << a << " = best; }\n";
           break;
-        case U_ADD: o << "  " << a << " = " << b << " + " << c << ";\n"; ovf(); break;
-        case U_SUB: o << "  " << a << " = " << b << " - " << c << ";\n"; ovf(); break;
-        case U_MUL: o << "  " << a << " = " << b << " * " << c << ";\n"; ovf(); break;
+        case U_ADD: arith(B + " + " + C); break;
+        case U_SUB: arith(B + " - " + C); break;
+        case U_MUL: arith(B + " * " + C); break;
         case U_DIV:
-          o << "  { const long long q = " << b << " / " << c << "; " << a << " = (" << b << " % " << c
+          o << "  { const long long q = " << B << " / " << C << "; " << a << " = (" << B << " % " << C
             << " != 0 && ((" << b << " < 0) != (" << c << " < 0))) ? q - 1 : q; }\n";
           break;
         case U_MOD:
-          o << "  { const long long m = " << b << " % " << c << "; " << a << " = m < 0 ? m + " << c << " : m; }\n";
+          o << "  { const long long m = " << B << " % " << C << "; " << a << " = m < 0 ? m + " << C << " : m; }\n";
           break;
-        case U_NEG: o << "  " << a << " = -" << b << ";\n"; ovf(); break;
+        case U_NEG: arith("-" + B); break;
         case U_EQ: o << "  " << a << " = " << b << " == " << c << ";\n"; break;
         case U_NE: o << "  " << a << " = " << b << " != " << c << ";\n"; break;
         case U_LT: o << "  " << a << " = " << b << " < " << c << ";\n"; break;
@@ -2139,18 +2177,13 @@ std::string user_device_source(const UserProg& P) {
         case U_NOT: o << "  " << a << " = !" << b << ";\n"; break;
         case U_AND: o << "  " << a << " = " << b << " & " << c << ";\n"; break;
         case U_OR: o << "  " << a << " = " << b << " | " << c << ";\n"; break;
-        case U_ADDI: o << "  " << a << " = " << b << " + " << in.imm << "LL;\n"; break;
+        case U_ADDI: o << "  " << a << " = " << B << " + " << in.imm << "LL;\n"; break;
         case U_BIT:
-          o << "  " << a << " = (" << c << " >= 1 && " << c << " <= 63) ? (" << b << " >> (" << c
+          o << "  " << a << " = (" << c << " >= 1 && " << c << " <= 63) ? (" << B << " >> (" << c
             << " - 1)) & 1 : 0;\n";
           break;
         case U_POPC: o << "  " << a << " = popcount64((u64)" << b << ");\n"; break;
-        case U_NTH:
-          o << "  { u64 m = (u64)" << b << "; long long j = " << c << ", pos = 0;\n"
-            << "    for (int p = 1; p <= 63 && m; ++p, m >>= 1)\n"
-            << "      if ((m & 1) && --j == 0) { pos = p; break; }\n"
-            << "    " << a << " = j > 0 || " << c << " < 1 ? 0 : pos; }\n";
-          break;
+        case U_NTH: o << "  " << a << " = ui_nth((u64)" << b << ", " << c << ");\n"; break;
         case U_MASK: o << "  " << a << " = (long long)((1ull << (" << b << " & 63)) - 1);\n"; break;
         case U_KIN:
           o << "  " << a << " = "

@@ -148,17 +148,7 @@ TLCG_HD int eval_user_v(const UserProg& P, int k, const V& v) {
       case U_ADDI: r[in.a] = r[in.b] + in.imm; break;
       case U_BIT: r[in.a] = (r[in.c] >= 1 && r[in.c] <= 63) ? (r[in.b] >> (r[in.c] - 1)) & 1 : 0; break;
       case U_POPC: r[in.a] = popcount64((u64)r[in.b]); break;
-      case U_NTH: {
-        u64 m = (u64)r[in.b];
-        long long j = r[in.c], pos = 0;
-        for (int p = 1; p <= 63 && m; ++p, m >>= 1)
-          if ((m & 1) && --j == 0) {
-            pos = p;
-            break;
-          }
-        r[in.a] = j > 0 || r[in.c] < 1 ? 0 : pos;
-        break;
-      }
+      case U_NTH: r[in.a] = ui_nth((u64)r[in.b], r[in.c]); break;
       case U_MASK: r[in.a] = (long long)((1ull << (r[in.b] & 63)) - 1); break;
       case U_KIN: {
         const int n = in.imm ? P.nv : P.nk;

@@ -71,7 +71,7 @@ def header(gpus=1):
     run_line = ("Running breadth-first search Model-Checking with 1 GPU (device 0) and seed 0." if gpus == 1 else
                 f"Running breadth-first search Model-Checking with {gpus} GPU ranks (FPSet partitioned by owner, "
                 f"rank r on device r mod 1) and seed 0.")
-    return ["tlc-hip: TLC-compatible breadth-first model checking on MI355X (libtlcgpu ABI 3)", run_line,
+    return ["tlc-hip: TLC-compatible breadth-first model checking on MI355X (libtlcgpu ABI 4)", run_line,
             "Parsing file compaction.tla (built-in: the definitions of compaction.tla this build implements)",
             "Semantic processing of module compaction", "Starting... (<DATE>)", "Computing initial states..."]
 
