@@ -2,7 +2,8 @@
 injected into compaction.tla, violated at depth) against the Python oracle's
 fixtures (tests/golden/user_inv.json, oracle/tla_eval.py): verdict, the
 violated invariant, depth, counts, TLC's counterexample trace text and TLC's
-counters at its stop point.  The global engine runs them in k_user_check;
+counters at its stop point.  The global engine runs them in its level check
+(tlcg_user_check, generated device code; k_user_check interprets with TLCG_JIT=0);
 the on-chip engines (component, component tree) run them as device code
 generated from the compiled program (user_inv.cpp user_device_source) inside
 their hipRTC-specialized kernels; the ranks of a multi-GPU check run them in
@@ -61,6 +62,28 @@ def test_user_invariant_check(case, order):
     else:
         check_path(m, r, want)
     ck.close()
+
+
+@pytest.mark.parametrize("jit", ["0", "1"])
+@pytest.mark.parametrize("case", ["U_LedgerCount", "U_all_hold", "U_ContextLedgerError", "U_mixed_user_first",
+                                  "U_producer_LedgerCount"])
+def test_user_invariant_global_check_kernel(case, jit, monkeypatch):
+    """the global engine's level check as hipRTC device code (tlcg_user_check,
+    jit_used bit 2) and as the interpreter (TLCG_JIT=0, k_user_check): the
+    same verdict, counts and TLC-order stop point"""
+    monkeypatch.setenv("TLCG_JIT", jit)
+    m = model(case)
+    want = GOLD[case]["result"]
+    ck = tlcgpu.Checker(m, tlc_order=True, engine="global")
+    st = ck.run_raw()
+    assert bool(st.jit_used & 4) == (jit == "1")
+    r = ck.run()
+    assert r.status == want["result"] and r.depth == want["depth"]
+    if want["result"] == "ok":
+        assert (r.generated, r.distinct) == (want["generated"], want["distinct"])
+    else:
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+        assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"])
 
 
 @pytest.mark.parametrize("case", sorted(GOLD))
