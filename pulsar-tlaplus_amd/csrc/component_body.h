@@ -90,11 +90,6 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 #ifndef TLCG_LVL_UNIFORM
 #define TLCG_LVL_UNIFORM 0
 #endif
-// per-level counts in LVL_COPIES interleaved copies (lane % copies), so the
-// 64 lanes' same-level adds hit 64 / copies to one address (A/B)
-#ifndef TLCG_LVL_COPIES
-#define TLCG_LVL_COPIES 1
-#endif
 // component codes: the invariants of both successors evaluated before their
 // FPSet probes, so the VALU work overlaps the probes' LDS round trips (a
 // successor found seen evaluated them in vain: 1.34 evaluations per new
@@ -170,11 +165,9 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
 #endif
   // per level: distinct states (low 32 bits) + successors generated by
   // expanding the level (high 32 bits), one packed 64-bit LDS add per lane and level
-  constexpr int LC = TLCG_LVL_COPIES;
-  __shared__ unsigned long long lvl_all[LV * LC];
-  unsigned long long* const lvl_sh = lvl_all + (LC > 1 ? lane % LC : 0);  // lvl_sh[l * LC]: level l, this lane's copy
+  __shared__ unsigned long long lvl_sh[LV];
   const int mb = L.msg_sh + L.N * L.mw;  // `messages` occupies the low mb bits
-  for (int i = lane; i < LV * LC; i += 64) lvl_all[i] = 0;
+  if (lane < LV) lvl_sh[lane] = 0;
   u64 gen = 0, dist = 0;
   unsigned od0 = 0, od1 = 0, od2 = 0;  // TLC's outdegree histogram: states with 0 / 1 / 2 new successors
   unsigned long long ev = NO_EVENT;
@@ -499,12 +492,12 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
             x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
             const unsigned s = (unsigned)__builtin_amdgcn_readlane((int)x, 15) + (unsigned)__builtin_amdgcn_readlane((int)x, 31) +
                                (unsigned)__builtin_amdgcn_readlane((int)x, 47) + (unsigned)__builtin_amdgcn_readlane((int)x, 63);
-            if (lane == 0) atomicAdd(&lvl_sh[lv0 * LC], (unsigned long long)(s & 0xFFFFu) | ((unsigned long long)(s >> 16) << 32));
+            if (lane == 0) atomicAdd(&lvl_sh[lv0], (unsigned long long)(s & 0xFFFFu) | ((unsigned long long)(s >> 16) << 32));
           } else {
-            atomicAdd(&lvl_sh[lvc * LC], lv);
+            atomicAdd(&lvl_sh[lvc], lv);
           }
 #else
-          atomicAdd(&lvl_sh[lvc * LC], lv);
+          atomicAdd(&lvl_sh[lvc], lv);
 #endif
         }
 #endif
@@ -529,7 +522,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       cur = head < tail0 ? nxt : first_new;  // position head was filled by this expansion
       if (head == lvl_end) {  // level `level` = [lvl_start, lvl_end) is complete, and expanded
 #ifndef TLCG_NO_LVL  // (experiment only: measures what the per-level counts cost)
-        if (level >= counted) atomicAdd(&lvl_sh[level * LC], (unsigned long long)(lvl_end - lvl_start) | ((unsigned long long)lvgen << 32));
+        if (level >= counted) atomicAdd(&lvl_sh[level], (unsigned long long)(lvl_end - lvl_start) | ((unsigned long long)lvgen << 32));
 #endif
         lgen += lvgen;
         lvgen = 0;
@@ -552,7 +545,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     } else if (act) {
       // the last level [lvl_start, tail) = [head, tail) was discovered, not
       // expanded (empty when the component ran out)
-      if (tail > lvl_start && level >= counted) atomicAdd(&lvl_sh[level * LC], (unsigned long long)(tail - lvl_start));
+      if (tail > lvl_start && level >= counted) atomicAdd(&lvl_sh[level], (unsigned long long)(tail - lvl_start));
       gen += lgen;
       dist += (u64)tail;
       if constexpr (OD) {
@@ -580,13 +573,9 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       if (o2) atomicAdd(&a.outdeg[so + 2], (unsigned long long)o2);
     }
   }
-  if (lane < LV) {
-    unsigned long long x = 0;  // (the copies' halves: < 2^32 each, so the packed sum does not carry)
-    for (int k = 0; k < LC; ++k) x += lvl_all[lane * LC + k];
-    if (x) {
-      atomicAdd(&a.lvl[so + lane], x & 0xffffffffull);
-      if (x >> 32) atomicAdd(&a.lvl_gen[so + lane], x >> 32);
-    }
+  if (lane < LV && lvl_sh[lane]) {
+    atomicAdd(&a.lvl[so + lane], lvl_sh[lane] & 0xffffffffull);
+    if (lvl_sh[lane] >> 32) atomicAdd(&a.lvl_gen[so + lane], lvl_sh[lane] >> 32);
   }
 }
 
