@@ -5,7 +5,8 @@
 CASE = name:cfg[:rank/world][|ENV=V,ENV2=V][|DEF=1;DEF2]
   cfg: s, m8, g9, g9deep, p8 (bench.py's CONFIGS)
   rank/world: a closed partition's share (e.g. 0/8: the first of 8 ranks)
-  ENV: environment for the run (TLCG_COMP_GRID=3072, TLCG_TREE_G=2, ...)
+  ENV: environment for the run (TLCG_COMP_GRID=3072, TLCG_TREE_G=2, ...;
+       PROBE_ENGINE=global, PROBE_TLC=1: TLC order)
   DEF: hipRTC define set (TLCG_JIT_DEFINES, e.g. TLCG_LDS_COLS=0)
 Each case builds its own context, runs 3 complete checks, and reports the
 best kernel time, the counts and the per-state cost (ps/state)."""
@@ -42,6 +43,7 @@ for spec in sys.argv[1:]:
     eng = os.environ.get("PROBE_ENGINE", "auto")  # (global: the HBM-FPSet engine, pre-sized)
     log2 = max(16, (2 * (c["distinct"] // world + 1) - 1).bit_length()) if eng == "global" else 0
     ck = T.Checker(m, rank=rank, world=world, engine=eng, log2_fpset_slots=log2,
+                   tlc_order=os.environ.get("PROBE_TLC", "0") == "1",
                    state_capacity=int(c["distinct"] * 1.15 / world) + (1 << 20))
     best, walls = 1e9, []
     for _ in range(reps):
