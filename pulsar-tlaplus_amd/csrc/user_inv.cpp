@@ -650,19 +650,25 @@ struct Val {
 
 struct Bind {
   bool by_name = true;  // an unevaluated expression (LET definition, operator argument)
+  bool own_env = false; // a LET definition: its environment is the one that holds it (not held
+                        // here, which would be a reference cycle)
   NodeP node;
   EnvP env;
   std::vector<std::string> params;
   Val v;                // by_name = false: a value in registers (bound variable)
 };
 
-struct Env {
+struct Env : std::enable_shared_from_this<Env> {
   std::map<std::string, Bind> m;
   EnvP up;
-  const Bind* find(const std::string& n) const {
+  // the binding of n, and (owner) the environment that holds it
+  const Bind* find(const std::string& n, const Env** owner = nullptr) const {
     for (const Env* e = this; e; e = e->up.get()) {
       auto it = e->m.find(n);
-      if (it != e->m.end()) return &it->second;
+      if (it != e->m.end()) {
+        if (owner) *owner = e;
+        return &it->second;
+      }
     }
     return nullptr;
   }
@@ -954,7 +960,7 @@ class Compiler {
         for (size_t i = 0; i < n->names.size(); ++i) {
           Bind b;
           b.node = n->c[i];
-          b.env = e;  // (LET definitions see each other, and themselves: recursion fails by depth)
+          b.own_env = true;  // (LET definitions see each other, and themselves: recursion fails by depth)
           b.params = n->params[i];
           e->m[n->names[i]] = b;
         }
@@ -1002,12 +1008,14 @@ class Compiler {
 
   // an identifier (or operator application) in scope
   Val name(const NodeP& n, const EnvP& env, const std::vector<NodeP>& args) {
-    if (const Bind* b = env->find(n->s)) {
+    const Env* owner = nullptr;
+    if (const Bind* b = env->find(n->s, &owner)) {
       if (!b->by_name) {
         if (!args.empty()) fail(n, n->s + " takes no arguments");
         return b->v;
       }
-      return substitute(n, b->node, b->env, b->params, args, env);
+      const EnvP benv = b->own_env ? std::const_pointer_cast<Env>(owner->shared_from_this()) : b->env;
+      return substitute(n, b->node, benv, b->params, args, env);
     }
     auto it = defs.find(n->s);
     if (it != defs.end()) {
