@@ -71,6 +71,12 @@ namespace tlcg {
 #ifndef TLCG_TREE_CAS1  // closed mode: the first CAS outside the probe loop; 0: inside (A/B)
 #define TLCG_TREE_CAS1 1
 #endif
+// (the same in Producer mode, where a collision then goes on to the loop:
+// P8 1.857-1.870 -> 1.824-1.826 ms, interleaved on one box,
+// profiles/r04_probe_cas1.jsonl; 0 for A/B)
+#ifndef TLCG_TREE_CAS1_OPEN
+#define TLCG_TREE_CAS1_OPEN 1
+#endif
 #ifndef TLCG_TREE_MULT  // the slot hash's multiplier (multiply-shift)
 #define TLCG_TREE_MULT 0x9E3779B1u
 #endif
@@ -178,9 +184,10 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         s = s >= (unsigned)TT ? s - (unsigned)TT : s;
       }
       int p0 = 0;
-      if constexpr (CLOSED && TLCG_TREE_CAS1) {
+      if constexpr (CLOSED ? TLCG_TREE_CAS1 : TLCG_TREE_CAS1_OPEN) {
         // the first CAS outside the probe loop: with the perfect hash it
-        // settles every insert, so the loop is skipped (no lane collides)
+        // settles every insert, so the loop is skipped (no lane collides);
+        // in Producer mode it settles most
         const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
         isnew = old == 0;
         p0 = old == 0 || old == key + 1u ? TT : 1;
