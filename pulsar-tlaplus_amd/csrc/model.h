@@ -217,9 +217,9 @@ TLCG_HD int highbit64(u64 x) {  // index of the highest set bit, x != 0
 // user_inv.h U_NTH: the 1-based position of the j-th set bit of m among bits
 // 1..63 (bit 64 excluded), 0 when j < 1 or m has fewer set bits
 TLCG_HD long long ui_nth(u64 m, long long j) {
-  // (a scan to the j-th set bit: in the specialized kernels this keeps G9 +
-  // LatestIsLast at 67 VGPRs, where clearing the lowest bits and a find-first
-  // takes 90 -- 5.42 vs 7.73 ms, profiles/r04_probe_uinv5.jsonl)
+  // (the interpreter's; the generated code uses ui_nth_n below.  A scan to
+  // the j-th set bit: clearing the lowest bits and a find-first took the
+  // specialized kernels from 67 to 90 VGPRs, profiles/r04_probe_uinv5.jsonl)
   const long long want = j;
   long long pos = 0;
   for (int p = 1; p <= 63 && m; ++p, m >>= 1)
@@ -228,6 +228,26 @@ TLCG_HD long long ui_nth(u64 m, long long j) {
       break;
     }
   return j > 0 || want < 1 ? 0 : pos;
+}
+
+// the same for the generated device code, where the layout is a constant: a
+// mask within the N message positions (every ledger and Len mask) is scanned
+// by N predicated steps, no loop; anything wider falls back to ui_nth.  G9 +
+// LatestIsLast 5.42 -> 4.88 ms (the built-in G9: 4.85), + LedgerSorted 24-38
+// -> 21.7, all six 47-56 -> 29.9 (profiles/r04_probe_nthn.jsonl)
+template <class LL>
+TLCG_HD long long ui_nth_n(const LL& L, u64 m, long long j) {
+  if (L.N <= 16 && (m >> L.N) == 0) {
+    long long pos = 0, cnt = 0;
+    for (int p = 1; p <= 16; ++p) {
+      if (p > L.N) break;
+      const long long b = (long long)((m >> (p - 1)) & 1);
+      cnt += b;
+      pos = b && cnt == j ? p : pos;
+    }
+    return j >= 1 ? pos : 0;
+  }
+  return ui_nth(m, j);
 }
 
 template <typename W>

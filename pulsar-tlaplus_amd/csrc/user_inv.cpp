@@ -2191,7 +2191,7 @@ std::string user_device_source(const UserProg& P) {
             << " - 1)) & 1 : 0;\n";
           break;
         case U_POPC: o << "  " << a << " = popcount64((u64)" << b << ");\n"; break;
-        case U_NTH: o << "  " << a << " = ui_nth((u64)" << b << ", " << c << ");\n"; break;
+        case U_NTH: o << "  " << a << " = ui_nth_n(v.L, (u64)" << b << ", " << c << ");\n"; break;
         case U_MASK: o << "  " << a << " = (long long)((1ull << (" << b << " & 63)) - 1);\n"; break;
         case U_KIN:
           o << "  " << a << " = "

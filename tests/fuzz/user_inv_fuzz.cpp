@@ -133,6 +133,19 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s CORPUS MUTANTS SEED\n", argv[0]);
     return 2;
   }
+  // the generated code's unrolled U_NTH (model.h ui_nth_n) against the
+  // interpreter's scan (ui_nth), exhaustively over N <= 10 and every mask
+  for (int n = 0; n <= 10; ++n) {
+    struct {
+      int N;
+    } lay{n};
+    for (uint64_t m = 0; m < (1ull << (n + 1)); ++m)  // (one bit past N: the fallback)
+      for (long long j = -1; j <= n + 2; ++j)
+        if (tlcg::ui_nth_n(lay, m, j) != tlcg::ui_nth(m, j)) {
+          std::fprintf(stderr, "ui_nth_n differs: N %d mask %llx j %lld\n", n, (unsigned long long)m, j);
+          return 1;
+        }
+  }
   const std::vector<Entry> corpus = read_corpus(argv[1]);
   const int mutants = std::atoi(argv[2]);
   Rng rng{std::strtoull(argv[3], nullptr, 10) | 1};
