@@ -196,3 +196,66 @@ def test_integer_overflow_is_an_evaluation_error():
     assert T.host_check_invariants(ok, s) == -1
     mul = T.Model(invariants=("Mul",), user_defs={"Mul": "65536 * 65536 + crashTimes >= 0"})
     assert T.host_check_invariants(mul, s) == 1
+
+
+# ---- differential mutation test: semantic mutants of every fixture body
+# (operators, quantifiers, connectives and literals swapped for others of
+# the same shape, so most stay in the language) compiled by the product and
+# by the oracle's independent evaluator, compared on every reachable state
+# of a small model wherever both accept the mutant
+_SWAPS = [(r"<=", ["<", ">="]), (r"(?<![<>=/\\|-])<(?![=>])", ["<=", ">"]), (r"(?<![=<>|-])>(?=[^=])", [">=", "<"]),
+          (r" # ", [" = "]), (r"(?<![=<>#/\\!|-])=(?![=>])", ["#"]), (r"/\\", ["\\/"]), (r"\\/", ["/\\"]),
+          (r"\\A ", ["\\E "]), (r"\\E ", ["\\A "]), (r"=>", ["/\\", "\\/"]), (r"\b\d+\b", None)]
+
+
+def _mutants(body, rng, n):
+    import re
+    out = []
+    for _ in range(n):
+        t = body
+        for _ in range(rng.randint(1, 2)):
+            pat, subs = _SWAPS[rng.randrange(len(_SWAPS))]
+            hits = list(re.finditer(pat, t))
+            if not hits:
+                continue
+            h = hits[rng.randrange(len(hits))]
+            if subs is None:  # an integer literal: k -> k +- 1, 0 or 2
+                k = int(h.group(0))
+                rep = str(rng.choice([k + 1, max(k - 1, 0), 0, 2]))
+            else:
+                rep = rng.choice(subs)
+            t = t[:h.start()] + rep + t[h.end():]
+        if t != body:
+            out.append(t)
+    return out
+
+
+def test_semantic_mutants_match_the_oracle():
+    import random
+    rng = random.Random(20261017)
+    kw = dict(msg_sent_limit=2, compaction_times_limit=2)
+    pairs = paired_states(T.Model(**kw))
+    words = [w for w, _ in pairs]
+    compared = disagreements = 0
+    bad = []
+    for name in sorted(CASES):
+        for body in _mutants(CASES[name], rng, 24):
+            defs = dict(HELPERS)
+            defs[name] = body
+            m = T.Model(invariants=(name,), user_defs=defs, **kw)
+            try:
+                got = T.host_check_invariants_batch(m, words)
+            except ValueError:
+                continue  # refused by the product (outside its subset, or a type error)
+            om = oracle_model(m)
+            try:
+                want = [oracle_code(om, [name], o) for _, o in pairs]
+            except Exception:  # noqa: BLE001  (outside the oracle evaluator's subset)
+                continue
+            compared += 1
+            diff = [(T.decode(T.Model(**kw), w), g, x) for (w, _), g, x in zip(pairs, got, want) if g != x]
+            if diff:
+                disagreements += 1
+                bad.append((name, body, diff[:2]))
+    assert not bad, (compared, bad[:3])
+    assert compared >= 100, compared
