@@ -197,3 +197,49 @@ def test_user_invariant_at_scale():
     assert (r.status, r.invariant, r.depth) == ("invariant", "LedgerCount", 12)
     # the per-message-sequence law (SURVEY App.A.1): every component reaches the same depth-12 level
     assert r.distinct % tlcgpu.init_count(m) == 0
+
+
+def _mutant_models():
+    """semantic mutants of every fixture (user_inv_cases.semantic_mutants),
+    those the product compiles, eight to a cfg's INVARIANTS list"""
+    import random
+    import sys
+    sys.path.insert(0, HERE)
+    from user_inv_cases import CASES, HELPERS, semantic_mutants
+    rng = random.Random(4)
+    defs, names = dict(HELPERS), []
+    for name in sorted(CASES):
+        for i, body in enumerate(semantic_mutants(CASES[name], rng, 8)):
+            mn = f"M{len(names)}"
+            trial = tlcgpu.Model(invariants=(mn,), user_defs={**HELPERS, mn: body})
+            if tlcgpu.check_model(trial):
+                continue  # refused (outside the supported subset)
+            defs[mn] = body
+            names.append(mn)
+    return [tlcgpu.Model(invariants=tuple(names[i:i + 8]), user_defs=defs) for i in range(0, len(names), 8)]
+
+
+@pytest.mark.parametrize("k", range(7))
+def test_semantic_mutants_device_code_matches_interpreter(k, monkeypatch):
+    """the generated device code in the component engine's kernel against the
+    interpreter (the global engine with TLCG_JIT=0, TLC order) on semantic
+    mutants of the fixtures, eight invariants a check: the same verdict,
+    invariant, depth, end-of-level counts, TLC-order trace and stop counters"""
+    models = _mutant_models()
+    if k >= len(models):
+        pytest.skip("fewer mutant groups")
+    m = models[k]
+    ck = tlcgpu.Checker(m)
+    a = ck.run()
+    stop_a = ck.tlc_stop_stats() if a.status != "ok" else None
+    ck.close()
+    monkeypatch.setenv("TLCG_JIT", "0")
+    ck = tlcgpu.Checker(m, tlc_order=True, engine="global")
+    b = ck.run()
+    stop_b = ck.tlc_stop_stats() if b.status != "ok" else None
+    ck.close()
+    assert a.engine == "component" and b.engine == "global"
+    assert (a.status, a.invariant, a.depth, a.generated, a.distinct) == \
+        (b.status, b.invariant, b.depth, b.generated, b.distinct)
+    if a.status != "ok":
+        assert a.trace == b.trace and stop_a == stop_b

@@ -8,7 +8,8 @@ import os
 
 import pytest
 
-from user_inv_cases import CASES, HELPERS, REF_TLA, T, model_with, oracle_model, paired_states, ref_definition
+from user_inv_cases import (CASES, HELPERS, REF_TLA, T, model_with, oracle_model, paired_states, ref_definition,
+                            semantic_mutants)
 
 
 def oracle_code(om, names, s):
@@ -199,37 +200,9 @@ def test_integer_overflow_is_an_evaluation_error():
 
 
 # ---- differential mutation test: semantic mutants of every fixture body
-# (operators, quantifiers, connectives and literals swapped for others of
-# the same shape, so most stay in the language) compiled by the product and
-# by the oracle's independent evaluator, compared on every reachable state
-# of a small model wherever both accept the mutant
-_SWAPS = [(r"<=", ["<", ">="]), (r"(?<![<>=/\\|-])<(?![=>])", ["<=", ">"]), (r"(?<![=<>|-])>(?=[^=])", [">=", "<"]),
-          (r" # ", [" = "]), (r"(?<![=<>#/\\!|-])=(?![=>])", ["#"]), (r"/\\", ["\\/"]), (r"\\/", ["/\\"]),
-          (r"\\A ", ["\\E "]), (r"\\E ", ["\\A "]), (r"=>", ["/\\", "\\/"]), (r"\b\d+\b", None)]
-
-
-def _mutants(body, rng, n):
-    import re
-    out = []
-    for _ in range(n):
-        t = body
-        for _ in range(rng.randint(1, 2)):
-            pat, subs = _SWAPS[rng.randrange(len(_SWAPS))]
-            hits = list(re.finditer(pat, t))
-            if not hits:
-                continue
-            h = hits[rng.randrange(len(hits))]
-            if subs is None:  # an integer literal: k -> k +- 1, 0 or 2
-                k = int(h.group(0))
-                rep = str(rng.choice([k + 1, max(k - 1, 0), 0, 2]))
-            else:
-                rep = rng.choice(subs)
-            t = t[:h.start()] + rep + t[h.end():]
-        if t != body:
-            out.append(t)
-    return out
-
-
+# (user_inv_cases.semantic_mutants) compiled by the product and by the
+# oracle's independent evaluator, compared on every reachable state of a
+# small model wherever both accept the mutant
 def test_semantic_mutants_match_the_oracle():
     import random
     rng = random.Random(20261017)
@@ -239,7 +212,7 @@ def test_semantic_mutants_match_the_oracle():
     compared = disagreements = 0
     bad = []
     for name in sorted(CASES):
-        for body in _mutants(CASES[name], rng, 24):
+        for body in semantic_mutants(CASES[name], rng, 24):
             defs = dict(HELPERS)
             defs[name] = body
             m = T.Model(invariants=(name,), user_defs=defs, **kw)

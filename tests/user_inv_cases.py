@@ -125,3 +125,33 @@ def ref_definition(name):
                 out.append(l2)
             return (m.group(1) or ""), "\n".join(out).rstrip()
     raise KeyError(name)
+
+
+# semantic mutants (tests/test_user_inv.py, tests/test_gpu_user_inv.py)
+_SWAPS = [(r"<=", ["<", ">="]), (r"(?<![<>=/\\|-])<(?![=>])", ["<=", ">"]), (r"(?<![=<>|-])>(?=[^=])", [">=", "<"]),
+          (r" # ", [" = "]), (r"(?<![=<>#/\\!|-])=(?![=>])", ["#"]), (r"/\\", ["\\/"]), (r"\\/", ["/\\"]),
+          (r"\\A ", ["\\E "]), (r"\\E ", ["\\A "]), (r"=>", ["/\\", "\\/"]), (r"\b\d+\b", None)]
+
+
+def semantic_mutants(body, rng, n):
+    """n seeded mutants of a definition body: an operator, connective,
+    quantifier or integer literal swapped for another of the same shape"""
+    import re
+    out = []
+    for _ in range(n):
+        t = body
+        for _ in range(rng.randint(1, 2)):
+            pat, subs = _SWAPS[rng.randrange(len(_SWAPS))]
+            hits = list(re.finditer(pat, t))
+            if not hits:
+                continue
+            h = hits[rng.randrange(len(hits))]
+            if subs is None:  # an integer literal: k -> k +- 1, 0 or 2
+                k = int(h.group(0))
+                rep = str(rng.choice([k + 1, max(k - 1, 0), 0, 2]))
+            else:
+                rep = rng.choice(subs)
+            t = t[:h.start()] + rep + t[h.end():]
+        if t != body:
+            out.append(t)
+    return out
