@@ -89,6 +89,18 @@ std::string program_source(const Layout& L, const std::string& user, bool check_
   return s;
 }
 
+// the compile options past -O3: TLCG_JIT_OPTS (tuning experiments), else the
+// machine scheduler's max-ILP strategy, which measured faster on every
+// specialized kernel (G9 4.74-4.77 -> 4.62-4.63 ms, M8 0.555 -> 0.546,
+// G9-deep 17.1 -> 16.4, P8 1.831 -> 1.820, G9 + a user invariant 4.91 ->
+// 4.79; interleaved on one box, profiles/r04_probe_sched2.jsonl).  The
+// precompiled global-engine kernels showed no steady gain from it (G9 88 / 95
+// vs 81 / 99 ms, M8 16.9 vs 17.2; r04_probe_sched_global.jsonl): not used there
+std::string jit_opts() {
+  const char* e = std::getenv("TLCG_JIT_OPTS");
+  return e ? e : "-mllvm -amdgpu-sched-strategy=max-ilp";
+}
+
 uint64_t fnv1a(const std::string& s) {
   uint64_t h = 1469598103934665603ull;
   for (unsigned char c : s) { h ^= c; h *= 1099511628211ull; }
@@ -124,11 +136,9 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
     return false;
   }
   const std::string a = "--offload-arch=" + arch;
-  std::vector<std::string> extra;  // tuning experiments: TLCG_JIT_OPTS="-mllvm -x=1 ..." (part of the cache key)
-  if (const char* e = std::getenv("TLCG_JIT_OPTS")) {
-    std::istringstream in(e);
-    for (std::string w; in >> w;) extra.push_back(w);
-  }
+  std::vector<std::string> extra;
+  std::istringstream in(jit_opts());
+  for (std::string w; in >> w;) extra.push_back(w);
   std::vector<const char*> opts = {a.c_str(), "-O3", "-std=c++20"};
   for (const std::string& w : extra) opts.push_back(w.c_str());
   const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
@@ -168,8 +178,7 @@ bool load_module(const Layout& L, int device, const std::string& user, bool chec
   arch = arch.substr(0, arch.find(':'));
   const std::string src = program_source(L, user, check_only);
   char key[64];
-  const char* jo = std::getenv("TLCG_JIT_OPTS");
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2" + (jo ? jo : "")));
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2" + jit_opts()));
   const std::string dir = cache_dir();
   const std::string path = dir + "/" + key + "-" + arch + ".co";
   std::vector<char> code;
