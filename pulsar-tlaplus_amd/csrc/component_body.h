@@ -93,16 +93,16 @@ struct CompShape { static constexpr int T = (K * TLCG_FPSET_NUM / TLCG_FPSET_DEN
 // component codes: the invariants of both successors evaluated before their
 // FPSet probes, so the VALU work overlaps the probes' LDS round trips (a
 // successor found seen evaluated them in vain: 1.34 evaluations per new
-// state instead of 1).  G9 4.84 -> 4.62 ms, M8 0.575 -> 0.546 ms
-// (profiles/r03_comp_spec_inv_ab.jsonl).  0: evaluated on insert -- the
-// default with user invariants, whose VALU work is more than the probes hide
-// (G9 + LatestIsLast 6.46 -> 5.42 ms, profiles/r04_probe_uinv.jsonl)
+// state instead of 1).  Round 3: G9 4.84 -> 4.62 ms, M8 0.575 -> 0.546 ms
+// (profiles/r03_comp_spec_inv_ab.jsonl).  Round 4, with the max-ILP
+// scheduler (jit.cpp jit_opts) the hiding no longer pays: evaluated on
+// insert, G9 4.65-4.69 -> 4.59 ms, G9's 1/8 share 0.645 -> 0.637, M8
+// 0.548-0.549 vs 0.550-0.555 (profiles/r04_probe_spec.jsonl); and with user
+// invariants, whose VALU work is more than the probes hide, it never paid
+// (G9 + LatestIsLast 6.46 -> 5.42 ms, r04_probe_uinv.jsonl).  1: before the
+// probes, for A/B
 #ifndef TLCG_SPEC_INV
-#ifdef TLCG_USER_INV
 #define TLCG_SPEC_INV 0
-#else
-#define TLCG_SPEC_INV 1
-#endif
 #endif
 // component codes: the queue entry behind the second successor's first FPSet
 // slot read before the first successor's probe (A/B)
