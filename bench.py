@@ -245,7 +245,7 @@ def cpu_baseline(cfg, seconds_target=12.0):
                 single_thread=single, wall_s=round(wall + wall_p, 2))
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -253,7 +253,93 @@ def main():
     ap.add_argument("--config", default="g9", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, one GPU per rank) or gloo (rehearsal)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_plan(gpus, environ):
+    """What `bench.py --gpus N` does in this environment:
+    ("run", None)      this process is the job's only rank, or one rank of a
+                       launched job (WORLD_SIZE set, equal to --gpus);
+    ("spawn", N)       no launcher ran: start N rank processes (spawn_ranks);
+    ("refuse", why)    --gpus contradicts the launcher's WORLD_SIZE."""
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: at least one rank"
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "refuse", (f"--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks: "
+                              f"the line would report {ws} GPUs under a --gpus {gpus} run")
+        return "run", None
+    return ("spawn", gpus) if gpus > 1 else ("run", None)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, child_argv, grace_s=90.0, environ=None):
+    """Start n rank processes of `child_argv` (one per GPU, LOCAL_RANK = rank),
+    the torch.distributed.run environment set for each, before this process
+    touches torch or a GPU (children, never a re-exec).  Rank 0's stdout is
+    this process's stdout (the JSON line); the other ranks' goes to stderr.
+    When a rank fails, the others get `grace_s` to finish (they are most
+    likely blocked in a collective with it) and are then terminated.
+    Returns the job's exit code: 0 if every rank exited 0, else the code of
+    the first rank that failed (the cause; the others' follow from it)."""
+    import signal
+    base = dict(os.environ if environ is None else environ)
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(child_argv, env=env, stdout=None if r == 0 else sys.stderr))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    first_bad, deadline = None, None
+    try:
+        while any(p.poll() is None for p in procs):
+            for r, p in enumerate(procs):
+                if first_bad is None and p.poll() not in (None, 0):
+                    first_bad = (r, p.returncode)
+                    deadline = time.time() + grace_s
+            if deadline is not None and time.time() > deadline:
+                stop()
+                deadline = time.time() + 30.0
+                for p in procs:
+                    try:
+                        p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+            time.sleep(0.05)
+    finally:
+        signal.signal(signal.SIGTERM, old)
+    for r, p in enumerate(procs):
+        if first_bad is None and p.returncode != 0:
+            first_bad = (r, p.returncode)
+    codes = [p.returncode for p in procs]
+    if first_bad is None:
+        return 0
+    r, rc = first_bad
+    print(f"bench: rank {r} of {n} failed first (exit {rc}); ranks' exit codes {codes}", file=sys.stderr, flush=True)
+    return rc if rc > 0 else 128 + (-rc)
+
+
+def main():
+    args = parse_args()
+    plan, what = launch_plan(args.gpus, os.environ)
+    if plan == "refuse":
+        print(f"bench: refused: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(what, [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]))
 
     import torch
     import tlcgpu
@@ -269,10 +355,16 @@ def main():
     if distributed:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
-        else:
-            dist.init_process_group(args.dist_backend)
+        try:
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+            else:
+                dist.init_process_group(args.dist_backend)
+        except Exception as e:  # noqa: BLE001
+            # e.g. RCCL's refusal of two ranks on one device (ncclCommInitRank: invalid usage)
+            print(f"bench: rank {rank}: {args.dist_backend} process group over {world} ranks on "
+                  f"{ndev} visible device(s) failed: {type(e).__name__}: {str(e)[:400]}", file=sys.stderr, flush=True)
+            sys.exit(4)
     dev = torch.device(f"cuda:{gpu}")
     rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # reduction tensors
 
@@ -531,17 +623,47 @@ def main():
             line["config"]["user_invariants"] = {n: USER_DEFS[n] for n in user_invariants(args.config)}
         if global_run:
             line["engines"]["global_hbm_fpset"] = summary(global_run)
+        if distributed:
+            line["dist_backend"] = args.dist_backend
+            line["rccl_ranks"] = preflight["rccl_ranks"] if preflight else None
+            if preflight:
+                line["rccl_preflight"] = preflight
         if exchange_run:
             line["engines"]["global_open_partition_alltoall"] = summary(exchange_run)
             line["exchange_leg_ok"] = True
+        elif exchange_error and exchange_error.startswith("skipped"):
+            line["exchange_leg_ok"] = None
+            line["exchange_leg_error"] = exchange_error
         elif exchange_error:
             line["engines"]["global_open_partition_alltoall"] = {"error": exchange_error}
             line["exchange_leg_ok"] = False
             line["exchange_leg_error"] = exchange_error
         return line
 
-    exchange_run = exchange_error = None
-    if distributed and not open_model and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
+    def rccl_preflight():
+        """The S cfg hash-partitioned on the whole state over the library's own
+        RCCL communicator (tlcg_comm_init -> tlcg_run_comm: all-gather, grouped
+        send/recv, all-reduce every level): exact counts, and the
+        communicator's rank count (tlcg_comm_size = ncclCommCount)"""
+        s_model = tlcgpu.Model()
+        eng = tdist.GpuEngine(s_model, rank, world, gpu, log2_fpset_slots=18, state_capacity=1 << 17,
+                              engine="global", partition=2)
+        try:
+            tdist.init_native(eng)
+            n = int(eng.lib.tlcg_comm_size(eng.ctx))
+            t = time.perf_counter()
+            r = tdist.run_native(eng)
+            ms = (time.perf_counter() - t) * 1e3
+        finally:
+            eng.close()
+        want = CONFIGS["s"]
+        ok = (r.generated, r.distinct, r.depth) == (want["generated"], want["distinct"], want["depth"])
+        return dict(rccl_ranks=n, counts_exact=ok, levels=r.depth, ms=round(ms, 2))
+
+    exchange_run = exchange_error = preflight = None
+    if distributed and not open_model and args.dist_backend != "nccl":
+        exchange_error = f"skipped: the exchange runs over RCCL, not {args.dist_backend} (a rehearsal backend)"
+    elif distributed and not open_model and os.environ.get("TLCG_BENCH_EXCHANGE", "1") != "0":
         # a secondary measurement (BASELINE config 4): its failure (every rank
         # learns of it through torch's own group) must not cost the headline
         # line, and neither may a hang -- the library aborts a collective after
@@ -550,17 +672,22 @@ def main():
         limit = float(os.environ.get("TLCG_BENCH_EXCHANGE_TIMEOUT_S", "240"))
 
         def bail():
-            # the headline line still stands; the hung leg is named at its top
-            # level (exchange_leg_ok false), never reported as a success
+            # the headline line still stands, but a hung leg is a failed job:
+            # it is named at the line's top level (exchange_leg_ok false) and
+            # the process exits non-zero
             if rank == 0:
                 print(json.dumps(build_line(None, f"the exchange leg did not finish within {limit:.0f} s")), flush=True)
-            os._exit(0)
+            print(f"bench: rank {rank}: the exchange leg hung (> {limit:.0f} s)", file=sys.stderr, flush=True)
+            os._exit(3)
 
         import threading
         watchdog = threading.Timer(limit, bail)
         watchdog.daemon = True
         watchdog.start()
         try:
+            preflight = rccl_preflight()
+            if not preflight["counts_exact"]:
+                raise RuntimeError(f"RCCL preflight on the S cfg: inexact counts {preflight}")
             exchange_run = time_exchange(2)
             ok = 1
         except (Exception, SystemExit) as e:  # noqa: BLE001

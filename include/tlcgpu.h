@@ -425,6 +425,9 @@ void tlcg_node_destroy(tlcg_node* node);
 int tlcg_comm_available(void);
 int tlcg_comm_unique_id(void* id, int32_t cap);
 int tlcg_comm_init(tlcg_ctx* c, const void* id, int32_t len);
+/* The rank count of the context's RCCL communicator (ncclCommCount), 0 when
+ * it has none: what a caller reports as the ranks the exchange really ran on. */
+int tlcg_comm_size(tlcg_ctx* c);
 int tlcg_run_comm(tlcg_ctx* c, tlcg_stats* st, uint64_t* levels, int32_t cap, int32_t* n_levels);
 
 /* TLC -checkpoint: write the run's committed levels (state store + parent

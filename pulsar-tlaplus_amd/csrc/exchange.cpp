@@ -32,6 +32,7 @@ struct Rccl {
   ncclResult_t (*CommDestroy)(ncclComm_t);
   ncclResult_t (*CommAbort)(ncclComm_t);
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*);
+  ncclResult_t (*CommCount)(const ncclComm_t, int*);
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
@@ -67,6 +68,7 @@ const Rccl* load_rccl(std::string* err) {
     sym(r.CommDestroy, "ncclCommDestroy");
     sym(r.CommAbort, "ncclCommAbort");
     sym(r.CommGetAsyncError, "ncclCommGetAsyncError");
+    sym(r.CommCount, "ncclCommCount");
     sym(r.AllGather, "ncclAllGather");
     sym(r.AllReduce, "ncclAllReduce");
     sym(r.Send, "ncclSend");
@@ -293,6 +295,14 @@ int comm_init_all(tlcg_ctx* const* ctxs, int n, std::string* err) {
   return 0;
 }
 
+int comm_size(tlcg_ctx* c) {
+  auto* s = static_cast<CommState*>(ctx_comm(c));
+  const Rccl* R = load_rccl(nullptr);
+  int n = 0;
+  if (!s || !s->comm || !R || R->CommCount(s->comm, &n) != ncclSuccess) return 0;
+  return n;
+}
+
 Transport* comm_transport(tlcg_ctx* c) {
   auto* s = static_cast<CommState*>(ctx_comm(c));
   return s && s->comm ? s->t.get() : nullptr;
@@ -436,7 +446,7 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
   std::memset(&s, 0, sizeof s);
   // TLCG_RANK_TRACE=1: per-phase wall time of this rank's loop on stderr
   const bool trace = std::getenv("TLCG_RANK_TRACE") != nullptr;
-  double ph[7] = {0, 0, 0, 0, 0, 0, 0};  // (unused), expand, counts, inbox, records, absorb, end_level
+  double ph[7] = {0, 0, 0, 0, 0, 0, 0};  // [1..6]: expand, counts, inbox, records, absorb, end_level
   auto clk = [] { return std::chrono::steady_clock::now(); };
   auto tick = [&](int i, std::chrono::steady_clock::time_point& t) {
     const auto n2 = clk();
@@ -530,9 +540,9 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
   }
   if (trace)
     std::fprintf(stderr,
-                 "rank %d: %d levels (%llu redone), wall s: flags %.3f expand %.3f counts %.3f inbox %.3f records %.3f "
+                 "rank %d: %d levels (%llu redone), wall s: expand %.3f counts %.3f inbox %.3f records %.3f "
                  "absorb %.3f end %.3f; device ms: kernels %.1f expand %.1f\n",
-                 me, nlev, (unsigned long long)s.levels_redone, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6],
+                 me, nlev, (unsigned long long)s.levels_redone, ph[1], ph[2], ph[3], ph[4], ph[5], ph[6],
                  s.kernel_ms, s.expand_ms);
   // ---- combine, like one context's level loop would report ----
   std::vector<uint64_t> mine(1u << 16), gen(1u << 16);
@@ -627,6 +637,8 @@ int tlcg_comm_init(tlcg_ctx* c, const void* id, int32_t len) {
   if (r) tlcg::ctx_set_error(c, err);
   return r;
 }
+
+int tlcg_comm_size(tlcg_ctx* c) { return c ? tlcg::comm_size(c) : 0; }
 
 int tlcg_run_comm(tlcg_ctx* c, tlcg_stats* st, uint64_t* levels, int32_t cap, int32_t* n_levels) {
   if (!c || !st) return -1;

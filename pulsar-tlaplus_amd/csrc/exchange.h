@@ -58,6 +58,7 @@ int comm_init(tlcg_ctx* c, const void* id, std::string* err);
 // one communicator per context, all devices distinct, one process (ncclCommInitAll)
 int comm_init_all(tlcg_ctx* const* ctxs, int n, std::string* err);
 Transport* comm_transport(tlcg_ctx* c);  // the context's RCCL transport, or null
+int comm_size(tlcg_ctx* c);              // ncclCommCount of the context's communicator, 0 if none
 void comm_free(void* comm_state);
 
 // the first error's counterexample walked across the ranks' stores (tlcgpu.hip;

@@ -59,8 +59,8 @@ namespace tlcg {
 // evaluation per expansion step, the depth's states spread over the group's
 // lanes) instead of when it is inserted (one per insert call, two per step
 // outside pair mode); every state is expanded once, at the depth after its
-// own, so the same states are checked and a violation still raises
-// TREE_EVENT (the global engine reports it); 0: at insert, for A/B
+// own, so the same states are checked and a violation still reaches the
+// least error key (a.event: tree_event_key); 0: at insert, for A/B
 // (_OPEN: Producer mode, where a component's entries are expanded too)
 #ifndef TLCG_TREE_INV_AT_EXPAND
 #define TLCG_TREE_INV_AT_EXPAND 1
@@ -420,14 +420,13 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
     if (__ballot(flags != 0)) break;  // the global engine takes the model
   }
   // fold the lanes' flags and the largest component, then the per-depth counts
-  const unsigned fl = __ballot(flags & TREE_EVENT) ? TREE_EVENT : 0;
   const unsigned fo = __ballot(flags & TREE_OVERFLOW) ? TREE_OVERFLOW : 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) maxn = max(maxn, (uint32_t)__shfl_xor(maxn, off));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) evk = min(evk, (u64)__shfl_xor((unsigned long long)evk, off));
   if (lane == 0) {
-    if (fl | fo) atomicOr(a.flags, fl | fo);
+    if (fo) atomicOr(a.flags, fo);
     atomicMax(a.max_n, maxn);
     if (evk != ~0ull) atomicMin(a.event, (unsigned long long)evk);
   }

@@ -224,10 +224,6 @@ int main(int argc, char** argv) {
   }
   char cerr[512];
   if (tlcg_check_model(&model, cerr, sizeof cerr) != 0) { std::printf("Error: %s\n", cerr); return 150; }
-  if (model.user_defs && o.gpus > 1) {  // user invariants run on one rank (include/tlcgpu.h)
-    std::fprintf(stderr, "tlc-hip: the cfg has invariants added to the module; checking on one GPU\n");
-    o.gpus = 1;
-  }
   const std::string recover_file = o.recover.empty() ? "" : o.recover + kCheckpointFile;
   if (!recover_file.empty()) {
     std::ifstream probe(recover_file, std::ios::binary);
@@ -472,6 +468,9 @@ int main(int argc, char** argv) {
       st.generated = sg;
       st.distinct = sd;
       stop_left = sq;
+    } else if (tctx) {
+      std::printf("Warning: TLC's counts at its stop could not be worked out (%s); the counts below are at the end "
+                  "of the level.\n", tlcg_last_error(tctx));
     }
     if (own) tlcg_destroy(tctx);
   }

@@ -145,6 +145,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_comm_available": (C.c_int, []),
         "tlcg_comm_unique_id": (C.c_int, [P, I32]),
         "tlcg_comm_init": (C.c_int, [P, P, I32]),
+        "tlcg_comm_size": (C.c_int, [P]),
         "tlcg_run_comm": (C.c_int, [P, S, C.POINTER(U64), I32, C.POINTER(I32)]),
         "tlcg_check_termination": (C.c_int, [M, O, I32, C.POINTER(tlcg_liveness), C.POINTER(U64),
                                              C.POINTER(I32), I32, C.POINTER(I32), C.c_char_p, I32]),

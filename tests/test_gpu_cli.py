@@ -160,19 +160,23 @@ def test_cli_termination_property(tmp_path):
     assert f"{want['generated']} states generated, {want['distinct']} distinct states found, 0 states left on queue." in lines
 
 
-def test_cli_injected_invariant(tmp_path):
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_cli_injected_invariant(tmp_path, gpus):
     """BASELINE config 5: an invariant added to the module (here with -defs, as
     the box has no .tla) and named in INVARIANTS, violated at depth 12: TLC's
     -workers 1 trace, its counts where it stops, exit code 12 -- the Python
-    oracle's fixture (tests/golden/user_inv.json, oracle/tla_eval.py)"""
+    oracle's fixture (tests/golden/user_inv.json, oracle/tla_eval.py).  With
+    -gpus 2 the check runs on two ranks (the added invariant on both, VERDICT
+    r4 item 2), and the report is the same TLC -workers 1 report."""
     import json
     from user_inv_cases import CASES
     g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "user_inv.json")))
     want = g["U_LedgerCount"]["result"]
     defs = tmp_path / "added.tla"
     defs.write_text("\\* an invariant the user adds\nLedgerCount == " + CASES["LedgerCount"] + "\n")
-    rc, lines = run(tmp_path, numeric_cfg(INVARIANTS="LedgerCount"), ["-defs", str(defs)])
-    expect = header() + ["Finished computing initial states: 729 distinct states generated at <DATE>.",
+    rc, lines = run(tmp_path, numeric_cfg(INVARIANTS="LedgerCount"),
+                    ["-defs", str(defs)] + (["-gpus", str(gpus)] if gpus > 1 else []))
+    expect = header(gpus) + ["Finished computing initial states: 729 distinct states generated at <DATE>.",
                          "Error: Invariant LedgerCount is violated.",
                          "Error: The behavior up to this point is:"]
     for i, t in enumerate(want["trace"]):
