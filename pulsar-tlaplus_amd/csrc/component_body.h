@@ -185,7 +185,12 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
     const u64 msgs = s0 & L.msgs_mask;
     const CompMsgs cmsg = comp_msgs_init(L, s0);  // everything that reads only `messages`
     CodeConsts ccon{};
-    if constexpr (CODE) ccon = code_consts(L, cmsg);
+    if constexpr (CODE) {
+      ccon = code_consts(L, cmsg);
+#ifdef TLCG_USER_INV
+      code_consts_user(L, ccon);  // the user invariants' outcome tables of this component
+#endif
+    }
     u64* st = a.store + b * (u64)K * 64 + (u64)lane;
     u64* par = a.parents + b * (u64)K * 64 + (u64)lane;
     const u64 gbase = a.store_base + b * (u64)K * 64 + (u64)lane;
@@ -230,7 +235,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       }
       lgen = 1;
       int c;
-      if constexpr (CODE) c = check_invariants_c(L, ccon, k0);
+      if constexpr (CODE) c = check_invariants_direct(L, ccon, k0);
       else c = check_invariants_k(L, cmsg, k0);
       if (c >= 0) {  // an initial state violates: level field 0 sorts before every expansion
         lev = make_comp_event(0, idx0, 0, 0, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1);
@@ -259,6 +264,8 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       return 0;
 #else
       if (TLCG_SPEC_INV && CODE) return pinv;  // (evaluated before the probe)
+      // (FLAT: the user invariants' tables; INV_UNKNOWN is settled in the rare branch)
+      if constexpr (CODE && TLCG_COMP_FLAT) return check_invariants_cbt(L, ccon, key) + 1;
       if constexpr (CODE) return check_invariants_cb(L, ccon, key) + 1;
       else return check_invariants_k(L, cmsg, key) + 1;
 #endif
@@ -457,13 +464,25 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       // events in one rare branch (with an action error and a deadlock, the
       // action error's key, action < 15, is the smaller)
       if ((r == 2) | (nsucc == 0 && L.check_deadlock) | (ev1 != 0) | (ev2 != 0)) {
+        if constexpr (CODE) {
+          // an outcome table left it to the programs (check_invariants_cbt):
+          // one inlined evaluation of both successors here
+#pragma nounroll
+          for (int i = 0; i < 2; ++i) {
+            if ((i ? ev2 : ev1) == INV_UNKNOWN + 1) {
+              const int e = check_invariants_direct(L, ccon, i ? t2 : t) + 1;
+              if (i) ev2 = e;
+              else ev1 = e;
+            }
+          }
+        }
         u64 k = r == 2 ? make_comp_event(level + 1, idx0, head, action, EVK_ACTION_ERROR, action)
                 : nsucc == 0 && L.check_deadlock ? make_comp_event(level + 1, idx0, head, 15, EVK_DEADLOCK, 0)
                                                  : NO_EVENT;
         if (ev1) k = min(k, make_comp_event(level + 1, idx0, head, action, ((ev1 - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION, (ev1 - 1) >> 1));
         if (ev2) k = min(k, make_comp_event(level + 1, idx0, head, ACT_CRASH, ((ev2 - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION, (ev2 - 1) >> 1));
         lev = min(lev, k);
-        stop = true;
+        stop = stop || k != NO_EVENT;  // (no event: every unknown outcome held)
       }
 #endif
 #if TLCG_COMP_FLAT

@@ -73,11 +73,13 @@ struct CodeConsts {
   int hz_false;   // ... and one of them has no witness in CompactMessages(messages, len)
   int dn0, dn1;   // DuplicateNullKeyMessage is FALSE at horizon 0 / len (ledger present)
   u64 msgs;       // the `messages` bits of the word (UVCode)
+  u64 utab;       // user invariants' per-component outcome tables (code_consts_user; 0 without)
 };
 
 TLCG_HD CodeConsts code_consts(const Layout& L, const CompMsgs& c) {
   CodeConsts k;
   k.msgs = c.msgs;
+  k.utab = 0;
   k.len = (uint32_t)c.len;
   const u64 cm = (c.len >= 1 && c.len <= L.N) ? (c.cm >> ((c.len - 1) * L.N)) & nmask(L.N) : 0;
   k.ledbits = (lkey)(1u | (cm << 1));
@@ -192,6 +194,108 @@ struct UVCode {
     return ((c >> (j - 1)) & 1) ? (u64)(K.ledbits >> 1) : 0ull;
   }
 };
+
+// The fields of a state a user invariant's program can read (user_inv.cpp
+// user_device_source finds them over the instructions reachable from its
+// entry): its code bits, below.  `messages` and Len(messages) are constants
+// of a component and take none.
+enum UserField : uint32_t {
+  UF_PH = 1, UF_R = 2, UF_H = 4, UF_X = 8, UF_CR = 16, UF_CP = 32, UF_CH = 64, UF_CC = 128, UF_LED = 256
+};
+TLCG_HD uint32_t code_field_mask(const Layout& L, uint32_t f) {
+  uint32_t m = 0;
+  if (f & UF_LED) m |= lmask(L.C);
+  if (f & UF_R) m |= 1u << cc_r(L);
+  if (f & UF_H) m |= 1u << cc_h(L);
+  if (f & UF_PH) m |= 7u << cc_ph(L);
+  if (f & UF_X) m |= lmask(L.ctx_w) << cc_x(L);
+  if (f & UF_CP) m |= 1u << cc_cp(L);
+  if (f & UF_CH) m |= 1u << cc_ch(L);
+  if (f & UF_CC) m |= lmask(L.curc_w) << cc_cc(L);
+  if (f & UF_CR) m |= lmask(L.cr_w) << cc_cr(L);
+  return m;
+}
+// the bits of c under mask m, packed (pext); and back (pdep).  Under hipRTC
+// m is a constant and the loops fold to a few shifts.
+TLCG_HD uint32_t code_pext(ckey c, uint32_t m) {
+  uint32_t r = 0;
+  int j = 0;
+  for (int b = 0; b < 32; ++b)
+    if ((m >> b) & 1u) r |= ((c >> b) & 1u) << j++;
+  return r;
+}
+TLCG_HD ckey code_pdep(uint32_t p, uint32_t m) {
+  ckey r = 0;
+  int j = 0;
+  for (int b = 0; b < 32; ++b)
+    if ((m >> b) & 1u) r |= ((p >> j++) & 1u) << b;
+  return r;
+}
+
+// UVCode that notes a read the code alone does not determine: a message
+// position outside 1..N or a ledger index outside 1..C reads the word
+template <typename W>
+struct UVTab : UVCode<W> {
+  mutable bool wide = false;
+  TLCG_HDM int key(int i) const { wide |= !(i >= 1 && i <= this->L.N); return UVCode<W>::key(i); }
+  TLCG_HDM int val(int i) const { wide |= !(i >= 1 && i <= this->L.N); return UVCode<W>::val(i); }
+  TLCG_HDM int ledp(int j) const { wide |= !(j >= 1 && j <= this->L.C); return UVCode<W>::ledp(j); }
+  TLCG_HDM u64 ledm(int j) const { wide |= !(j >= 1 && j <= this->L.C); return UVCode<W>::ledm(j); }
+};
+
+#ifdef TLCG_USER_INV
+// Outcome tables of the user invariants (round 5).  Inside a component
+// `messages` is a constant, so a user invariant's outcome on a code depends
+// only on the code bits of the fields its program reads (tlcg_user_tab_mask)
+// and on the component constants it reads.  With at most 4 such bits, the
+// outcomes of every pattern of them sit in CodeConsts::utab (2 bits per
+// pattern, from bit tlcg_user_tab_off), and each state reads its outcome
+// there instead of running the program:
+//   - an invariant that reads of the component constants at most Len and the
+//     ledger content (CodeConsts len, ledbits) has its tables worked out on
+//     the host when the kernels are generated, one per value of the two
+//     (tlcg_user_tab_static: a constant array);
+//   - one that reads `messages` has its table filled when the component
+//     starts, one evaluation per pattern (tlcg_user_tab_dyn).
+// An evaluation that read something its pattern and class do not fix
+// (UVTab::wide) leaves the value 3, and the states with that pattern run the
+// program themselves: the tables are exact on every code.  The four
+// tlcg_user_tab_* are generated with the invariants (user_inv.cpp
+// user_device_source, which also finds what each program reads).
+TLCG_HD int tlcg_user_tab_off(int k);        // bit offset of k's table in utab, or -1 (none)
+TLCG_HD uint32_t tlcg_user_tab_mask(int k);  // the code bits k's table is indexed by
+TLCG_HD int tlcg_user_tab_dyn(int k);        // 1: k's table is filled per component
+TLCG_HD u64 tlcg_user_tab_static(const CodeConsts& K);  // the host-made tables of K's class
+
+template <typename W = u64>
+TLCG_HD void code_consts_user(const Layout& L, CodeConsts& K) {
+  K.utab = tlcg_user_tab_static(K);
+  for (int q = 0; q < L.n_inv; ++q) {
+    if (L.inv[q] < INV_USER) continue;
+    const int k = L.inv[q] - INV_USER;
+    const int off = tlcg_user_tab_off(k);
+    if (off < 0 || !tlcg_user_tab_dyn(k)) continue;
+    const uint32_t m = tlcg_user_tab_mask(k);
+    const int np = 1 << popcount32(m);
+    for (int p = 0; p < np; ++p) {
+      const UVTab<W> v{{L, K, code_pdep((uint32_t)p, m)}};
+      const int r = tlcg_user_eval(k, v);
+      K.utab |= (u64)(v.wide ? 3 : r) << (off + 2 * p);
+    }
+  }
+}
+
+// user invariant k on code c: its table, else its program
+template <typename W = u64>
+TLCG_HD int user_eval_c(const Layout& L, const CodeConsts& K, int k, ckey c) {
+  const int off = tlcg_user_tab_off(k);
+  if (off >= 0) {
+    const int e = (int)((K.utab >> (off + 2 * (int)code_pext(c, tlcg_user_tab_mask(k)))) & 3u);
+    if (e != 3) return e;
+  }
+  return tlcg_user_eval(k, UVCode<W>{L, K, c});
+}
+#endif
 
 TLCG_HD int c_phase(const Layout& L, ckey c) { return (int)cget(c, cc_ph(L), 3); }
 // MaxCompactedLedgerId, compaction.tla:103-106
@@ -348,7 +452,7 @@ TLCG_HD int check_invariants_c(const Layout& L, const CodeConsts& K, ckey c) {
       default:
         r = EV_ERROR;
 #ifdef TLCG_USER_INV
-        if (L.inv[q] >= INV_USER) r = tlcg_user_eval(L.inv[q] - INV_USER, UVCode<W>{L, K, c});
+        if (L.inv[q] >= INV_USER) r = user_eval_c<W>(L, K, L.inv[q] - INV_USER, c);
 #endif
     }
     if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
@@ -373,11 +477,71 @@ TLCG_HD int check_invariants_cb(const Layout& L, const CodeConsts& K, ckey c) {
     if (L.inv[q] == INV_HORIZON) r = horizon;
     if (L.inv[q] == INV_DUPNULL) r = dupnull;
 #ifdef TLCG_USER_INV
-    if (L.inv[q] >= INV_USER) r = tlcg_user_eval(L.inv[q] - INV_USER, UVCode<W>{L, K, c});
+    if (L.inv[q] >= INV_USER) r = user_eval_c<W>(L, K, L.inv[q] - INV_USER, c);
 #endif
     if (r != EV_TRUE) res = (q << 1) | (r == EV_ERROR ? 1 : 0);
   }
   return res;
+}
+
+// check_invariants_cb for the component kernel's inserts (round 5): the user
+// invariants read from their outcome tables only, and a table entry that
+// leaves the decision to the program (3, rare) makes the whole answer
+// INV_UNKNOWN, which the kernel settles once, in its rare branch, with
+// check_invariants_direct.  So the programs are inlined there once instead
+// of into every insert (with six user invariants the copies spilled the
+// kernel's scalar registers: G9 18.4 ms against 4.9-5.0 with any one of them).
+constexpr int INV_UNKNOWN = 0x3FFE;
+template <typename W = u64>
+TLCG_HD int check_invariants_cbt(const Layout& L, const CodeConsts& K, ckey c) {
+#ifdef TLCG_USER_INV
+  const uint32_t hb = (c >> cc_h(L)) & 1;
+  const uint32_t X = cget(c, cc_x(L), L.ctx_w);
+  const bool ctx_ok = X >= 1 && (int)X <= L.C && ((c >> (X - 1)) & 1);
+  const int horizon = (!hb || K.len == 0 || !K.hz_live) ? EV_TRUE : !ctx_ok ? EV_ERROR : K.hz_false ? EV_FALSE : EV_TRUE;
+  const int dupnull = !(L.retain && X != 0) ? EV_TRUE : !ctx_ok ? EV_ERROR : (hb ? K.dn1 : K.dn0) ? EV_FALSE : EV_TRUE;
+  int res = -1;
+  bool unknown = false;
+  for (int q = L.n_inv - 1; q >= 0; --q) {
+    int r = EV_ERROR;
+    if (L.inv[q] == INV_TYPESAFE) r = inv_typesafe_c(L, K, c);
+    if (L.inv[q] == INV_LEAK) r = inv_leak_c(L, c);
+    if (L.inv[q] == INV_HORIZON) r = horizon;
+    if (L.inv[q] == INV_DUPNULL) r = dupnull;
+    if (L.inv[q] >= INV_USER) {
+      const int k = L.inv[q] - INV_USER;
+      const int off = tlcg_user_tab_off(k);
+      const int e = off >= 0 ? (int)((K.utab >> (off + 2 * (int)code_pext(c, tlcg_user_tab_mask(k)))) & 3u) : 3;
+      unknown |= e == 3;
+      r = e == 3 ? EV_TRUE : e;
+    }
+    if (r != EV_TRUE) res = (q << 1) | (r == EV_ERROR ? 1 : 0);
+  }
+  return unknown ? INV_UNKNOWN : res;
+#else
+  return check_invariants_cb<W>(L, K, c);
+#endif
+}
+
+// every invariant in cfg order, the user's by their programs (no tables)
+template <typename W = u64>
+TLCG_HD int check_invariants_direct(const Layout& L, const CodeConsts& K, ckey c) {
+  for (int q = 0; q < L.n_inv; ++q) {
+    int r;
+    switch (L.inv[q]) {
+      case INV_TYPESAFE: r = inv_typesafe_c(L, K, c); break;
+      case INV_LEAK: r = inv_leak_c(L, c); break;
+      case INV_HORIZON: r = inv_horizon_c(L, K, c); break;
+      case INV_DUPNULL: r = inv_dupnull_c(L, K, c); break;
+      default:
+        r = EV_ERROR;
+#ifdef TLCG_USER_INV
+        if (L.inv[q] >= INV_USER) r = tlcg_user_eval(L.inv[q] - INV_USER, UVCode<W>{L, K, c});
+#endif
+    }
+    if (r != EV_TRUE) return (q << 1) | (r == EV_ERROR ? 1 : 0);
+  }
+  return -1;
 }
 
 }  // namespace tlcg

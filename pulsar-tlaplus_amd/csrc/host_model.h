@@ -29,7 +29,18 @@ bool compile_user_invariants(const tlcg_model& m, const HostModel& hm, const std
 std::vector<std::string> user_def_names(const char* text);
 // The compiled user invariants as device code for the run-time specialized
 // kernels (user_inv.cpp; model.h tlcg_user_eval), one function per invariant.
-std::string user_device_source(const UserProg& P);
+// With the layout: the per-component outcome tables of the invariants that
+// read few code bits (component_code.h code_consts_user).
+std::string user_device_source(const UserProg& P, const Layout& L);
+// what user invariant k's program reads: the state fields (component_code.h
+// UserField), the component constants (user_inv.cpp UserConstRead), and its
+// host-made outcome table for one class (Len, ledger content mask) over the
+// code bits `mask` (2 bits per pattern, 3 = the program decides)
+uint32_t user_fields(const UserProg& P, int k);
+uint32_t user_const_reads(const UserProg& P, int k);
+// (P with its dead instructions replaced by loads of 0: user_static_table's input)
+UserProg user_prune_dead(const UserProg& P);
+u64 user_static_table(const UserProg& P, const Layout& L, int k, uint32_t mask, int len, uint32_t cm);
 
 // The FPSet slot-hash multiplier (multiply-shift over a T-slot table, linear
 // probing) with the fewest probe-loop trips on the insert sequence of the

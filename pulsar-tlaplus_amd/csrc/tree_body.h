@@ -259,6 +259,9 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         msgs = s0 & messages_mask<W>(L);
         cm = comp_msgs_init(L, (u64)s0);  // (`messages` sits in the low word)
         kc = code_consts(L, cm);
+#ifdef TLCG_USER_INV
+        code_consts_user<W>(L, kc);  // the user invariants' outcome tables of this component
+#endif
         if (code_word<W>(L, kc, msgs, code_encode_w<W>(L, s0)) != s0) flags |= TREE_OVERFLOW;  // no code
       } else {
         if (a.layer == 0) {

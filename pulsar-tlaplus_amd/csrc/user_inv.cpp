@@ -42,6 +42,7 @@
 #include <string>
 #include <vector>
 
+#include "component_code.h"
 #include "host_model.h"
 
 namespace tlcg {
@@ -2103,7 +2104,175 @@ std::string member_expr(const int32_t* t, int n, const std::string& x) {
 
 }  // namespace
 
-std::string user_device_source(const UserProg& P) {
+// What user invariant k's program reads of a state (user_fields: component_code.h
+// UserField bits; the component constants: UR_LEN, UR_MSGS, UR_LEDB), over the
+// instructions reachable from its entry whose result is used.  The lowering
+// builds every message record whole (position, key, value), so a program that
+// compares ids only still holds dead key / value reads; a backward liveness
+// pass over the register program drops those (an instruction is kept when it
+// can end the program -- a jump, a return, an error, an overflow check -- or
+// when a kept instruction reads its result).
+enum UserConstRead : uint32_t { UR_LEN = 1, UR_MSGS = 2, UR_LEDB = 4 };
+
+namespace {
+
+struct InsnRegs {
+  uint64_t use = 0, def = 0;
+  bool effect = false;  // ends the program or changes control: always kept
+};
+
+InsnRegs insn_regs(const UInsn& in) {
+  InsnRegs r;
+  const uint64_t A = 1ull << in.a, B = 1ull << in.b, C = 1ull << in.c;
+  switch (in.op) {
+    case U_LDI: case U_LEN: case U_PHASE: case U_P1R: case U_HZ: case U_CTX: case U_CRASH: case U_CURP: case U_CURH:
+    case U_CURC:
+      r.def = A;
+      break;
+    case U_MOV: case U_MKEY: case U_MVAL: case U_LEDP: case U_LEDM: case U_NOT: case U_ADDI: case U_POPC: case U_MASK:
+    case U_KIN: case U_KAT:
+      r.def = A;
+      r.use = B;
+      break;
+    case U_NEG:
+      r.def = A;
+      r.use = B;
+      r.effect = true;  // (the 32-bit overflow error)
+      break;
+    case U_ADD: case U_SUB: case U_MUL:
+      r.def = A;
+      r.use = B | C;
+      r.effect = true;
+      break;
+    case U_LFK: case U_DIV: case U_MOD: case U_EQ: case U_NE: case U_LT: case U_LE: case U_AND: case U_OR: case U_BIT:
+    case U_NTH:
+      r.def = A;
+      r.use = B | C;
+      break;
+    case U_JZ: case U_JNZ: case U_RET:
+      r.use = A;
+      r.effect = true;
+      break;
+    default:  // U_JMP, U_ERR, unknown
+      r.effect = true;
+      break;
+  }
+  return r;
+}
+
+std::vector<int> insn_succ(const UserProg& P, int pc) {
+  const UInsn& in = P.ins[pc];
+  if (in.op == U_RET || in.op == U_ERR) return {};
+  if (in.op == U_JMP) return {in.imm};
+  std::vector<int> s{pc + 1};
+  if (in.op == U_JZ || in.op == U_JNZ) s.push_back(in.imm);
+  return s;
+}
+
+// the instructions of P whose effect or result can matter (liveness to a fixpoint)
+std::vector<bool> needed_insns(const UserProg& P) {
+  const int n = P.n_ins;
+  std::vector<uint64_t> live_in((size_t)n + 1, 0);
+  std::vector<bool> need((size_t)n, false);
+  for (bool changed = true; changed;) {
+    changed = false;
+    for (int i = n - 1; i >= 0; --i) {
+      uint64_t out = 0;
+      for (int t : insn_succ(P, i))
+        if (t >= 0 && t <= n) out |= live_in[(size_t)t];
+      const InsnRegs r = insn_regs(P.ins[i]);
+      const bool nd = r.effect || (r.def & out);
+      const uint64_t in = nd ? (r.use | (out & ~r.def)) : out;
+      if (in != live_in[(size_t)i] || nd != need[(size_t)i]) {
+        live_in[(size_t)i] = in;
+        need[(size_t)i] = nd;
+        changed = true;
+      }
+    }
+  }
+  return need;
+}
+
+// fields (UserField) and component constants (UserConstRead) read by the
+// needed instructions reachable from invariant k's entry
+void user_reads(const UserProg& P, const std::vector<bool>& need, int k, uint32_t* fields, uint32_t* consts) {
+  const int n = P.n_ins;
+  std::vector<bool> seen((size_t)n + 1, false);
+  std::vector<int> todo{P.entry[k]};
+  uint32_t f = 0, c = 0;
+  while (!todo.empty()) {
+    const int pc = todo.back();
+    todo.pop_back();
+    if (pc < 0 || pc >= n || seen[(size_t)pc]) continue;
+    seen[(size_t)pc] = true;
+    for (int t : insn_succ(P, pc)) todo.push_back(t);
+    if (!need[(size_t)pc]) continue;
+    switch (P.ins[pc].op) {
+      case U_PHASE: f |= UF_PH; break;
+      case U_P1R: f |= UF_R; c |= UR_LEN; break;
+      case U_HZ: f |= UF_H; c |= UR_LEN; break;
+      case U_CTX: f |= UF_X; break;
+      case U_CRASH: f |= UF_CR; break;
+      case U_CURP: f |= UF_CP; break;
+      case U_CURH: f |= UF_CP | UF_CH; c |= UR_LEN; break;
+      case U_CURC: f |= UF_CP | UF_CC; break;
+      case U_LEDP: f |= UF_LED; break;
+      case U_LEDM: f |= UF_LED; c |= UR_LEDB; break;
+      case U_LEN: c |= UR_LEN; break;
+      case U_MKEY: case U_MVAL: case U_LFK: c |= UR_MSGS; break;
+      default: break;
+    }
+  }
+  *fields = f;
+  *consts = c;
+}
+
+// the class view of the host-made tables: a code and the two constants of a
+// class (len, ledbits); any read of `messages` is a read the class does not
+// fix (wide), as are UVTab's out-of-range positions
+struct UVClass : UVTab<u64> {
+  int key(int i) const { wide = true; return UVTab<u64>::key(i); }
+  int val(int i) const { wide = true; return UVTab<u64>::val(i); }
+};
+
+}  // namespace
+
+uint32_t user_fields(const UserProg& P, int k) {
+  uint32_t f = 0, c = 0;
+  user_reads(P, needed_insns(P), k, &f, &c);
+  return f;
+}
+
+uint32_t user_const_reads(const UserProg& P, int k) {
+  uint32_t f = 0, c = 0;
+  user_reads(P, needed_insns(P), k, &f, &c);
+  return c;
+}
+
+UserProg user_prune_dead(const UserProg& P) {
+  UserProg Q = P;
+  const std::vector<bool> need = needed_insns(P);
+  for (int i = 0; i < P.n_ins; ++i)
+    if (!need[(size_t)i]) Q.ins[i] = UInsn{(uint8_t)U_LDI, P.ins[i].a, 0, 0, 0};  // (its result is never read)
+  return Q;
+}
+
+u64 user_static_table(const UserProg& P, const Layout& L, int k, uint32_t mask, int len, uint32_t cm) {
+  CodeConsts K{};
+  K.len = (uint32_t)len;
+  K.ledbits = (lkey)(1u | (cm << 1));
+  K.msgs = 0;
+  if (popcount32(mask) > 5) return ~0ull;  // (more patterns than 64 bits hold: the programs decide)
+  u64 t = 0;
+  for (int p = 0; p < (1 << popcount32(mask)); ++p) {
+    const UVClass v{{{L, K, code_pdep((uint32_t)p, mask)}}};
+    const int r = eval_user_v(P, k, v);
+    t |= (u64)(v.wide ? 3 : r) << (2 * p);
+  }
+  return t;
+}
+
+std::string user_device_source(const UserProg& P, const Layout& L) {
   std::ostringstream o;
   o << "namespace tlcg {\n";
   const int n = P.n_ins;
@@ -2214,7 +2383,75 @@ std::string user_device_source(const UserProg& P) {
   }
   o << "template <class V>\nTLCG_HD int tlcg_user_eval(int k, const V& v) {\n  switch (k) {\n";
   for (int k = 0; k < P.n_user; ++k) o << "    case " << k << ": return tlcg_user_inv_" << k << "(v);\n";
-  o << "  }\n  return EV_ERROR;\n}\n}  // namespace tlcg\n";
+  o << "  }\n  return EV_ERROR;\n}\n";
+  // the outcome tables (component_code.h code_consts_user): an invariant whose
+  // program reads at most UTAB_BITS code bits gets 2 bits per pattern of them
+  // in CodeConsts::utab, while its 64 bits last; worked out here for every
+  // class (Len, ledger content) when it reads no `messages`, else per
+  // component on the device.  TLCG_UTAB=0: none (every state runs the
+  // programs; A/B and tests); TLCG_UTAB=dyn: no host-made ones;
+  // TLCG_UTAB=slow: every entry 3 (tests: every state takes the kernel's
+  // fallback evaluation).
+  constexpr int UTAB_BITS = 4;
+  const char* ut = std::getenv("TLCG_UTAB");
+  const bool tables = !(ut && ut[0] == '0');
+  const bool slow = ut && std::string(ut) == "slow";
+  const bool statics = !(ut && std::string(ut) == "dyn");
+  const std::vector<bool> need = needed_insns(P);
+  const UserProg pruned = user_prune_dead(P);  // (the class tables run it: no dead `messages` reads)
+  std::vector<int> off((size_t)P.n_user, -1), dyn((size_t)P.n_user, 0);
+  std::vector<uint32_t> mask((size_t)P.n_user, 0);
+  int used = 0;
+  for (int k = 0; k < P.n_user && tables; ++k) {
+    uint32_t f = 0, c = 0;
+    user_reads(P, need, k, &f, &c);
+    const uint32_t m = code_field_mask(L, f);
+    const int bits = popcount32(m);
+    if (bits > UTAB_BITS || used + (2 << bits) > 64) continue;
+    off[(size_t)k] = used;
+    mask[(size_t)k] = m;
+    dyn[(size_t)k] = ((c & UR_MSGS) || !statics || L.N > 8) && !slow ? 1 : 0;
+    used += 2 << bits;
+  }
+  o << "TLCG_HD int tlcg_user_tab_off(int k) {\n  switch (k) {\n";
+  for (int k = 0; k < P.n_user; ++k) o << "    case " << k << ": return " << off[(size_t)k] << ";\n";
+  o << "  }\n  return -1;\n}\n";
+  o << "TLCG_HD uint32_t tlcg_user_tab_mask(int k) {\n  switch (k) {\n";
+  for (int k = 0; k < P.n_user; ++k) o << "    case " << k << ": return " << mask[(size_t)k] << "u;\n";
+  o << "  }\n  return 0u;\n}\n";
+  o << "TLCG_HD int tlcg_user_tab_dyn(int k) {\n  switch (k) {\n";
+  for (int k = 0; k < P.n_user; ++k) o << "    case " << k << ": return " << dyn[(size_t)k] << ";\n";
+  o << "  }\n  return 0;\n}\n";
+  // the host-made tables: class (len, cm) at index len << N | cm, cm the
+  // ledger content's position mask (CodeConsts ledbits >> 1); a class past
+  // them (none is reachable: Len(messages) <= N) reads all 3s
+  u64 smask = 0;
+  for (int k = 0; k < P.n_user; ++k)
+    if (off[(size_t)k] >= 0 && !dyn[(size_t)k])
+      smask |= (((2 << popcount32(mask[(size_t)k])) >= 64 ? ~0ull : (1ull << (2 << popcount32(mask[(size_t)k]))) - 1)
+               << off[(size_t)k]);
+  if (!smask) {
+    o << "TLCG_HD u64 tlcg_user_tab_static(const CodeConsts&) { return 0; }\n";
+  } else if (slow) {
+    o << "TLCG_HD u64 tlcg_user_tab_static(const CodeConsts&) { return " << smask << "ull; }\n";
+  } else {
+    const int ncls = (L.N + 1) << L.N;
+    o << "__constant__ const u64 kUTabStatic[" << ncls << "] = {";
+    for (int len = 0; len <= L.N; ++len)
+      for (uint32_t cm = 0; cm < (1u << L.N); ++cm) {
+        u64 t = 0;
+        for (int k = 0; k < P.n_user; ++k)
+          if (off[(size_t)k] >= 0 && !dyn[(size_t)k])
+            t |= user_static_table(pruned, L, k, mask[(size_t)k], len, cm) << off[(size_t)k];
+        o << t << "ull" << (len == L.N && cm + 1 == (1u << L.N) ? "" : ", ");
+      }
+    o << "};\n";
+    o << "TLCG_HD u64 tlcg_user_tab_static(const CodeConsts& K) {\n"
+      << "  const uint32_t cm = (uint32_t)(K.ledbits >> 1);\n"
+      << "  return K.len <= " << L.N << "u && cm < " << (1u << L.N) << "u ? kUTabStatic[(K.len << " << L.N
+      << ") | cm] : " << smask << "ull;\n}\n";
+  }
+  o << "}  // namespace tlcg\n";
   return o.str();
 }
 

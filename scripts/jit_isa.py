@@ -1,0 +1,29 @@
+"""Diagnostics (CPU, no GPU): write the hipRTC source of the kernels
+specialized for a cfg (TLCG_JIT_DUMP) and compile it offline with hipcc to
+gfx950 assembly, so the ISA of the specialized kernels can be read.
+
+    python scripts/jit_isa.py [keys] [out_prefix]   -> out_prefix.hip, out_prefix.s
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pulsar-tlaplus_amd", "python"))
+import tlcgpu  # noqa: E402
+
+k = int(sys.argv[1]) if len(sys.argv) > 1 else 15
+out = sys.argv[2] if len(sys.argv) > 2 else "/tmp/g9jit"
+os.environ["TLCG_JIT_DUMP"] = out + ".hip"
+os.environ["TLCG_JIT_CACHE"] = "/tmp/tlcg-jit-isa-nocache"
+m = tlcgpu.Model(key_space=range(1, k + 1), value_space=range(1, k + 1))
+cm = m.to_c()
+err = C.create_string_buffer(8192)
+n = tlcgpu.load_library().tlcg_jit_selftest(C.byref(cm), b"gfx950", err, 8192)
+if n < 0:
+    raise SystemExit(err.value.decode())
+opts = os.environ.get("TLCG_JIT_OPTS", "-mllvm -amdgpu-sched-strategy=max-ilp").split()
+subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-x", "hip", "--cuda-device-only",
+                "-S", "-o", out + ".s", out + ".hip"] + opts, check=True)
+print(out + ".s")

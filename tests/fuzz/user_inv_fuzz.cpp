@@ -23,6 +23,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "component_code.h"
 #include "host_model.h"
 
 namespace {
@@ -158,6 +159,7 @@ int main(int argc, char** argv) {
   }
   const std::vector<uint64_t> states = reachable(base);
   long compiled = 0, refused = 0, evals = 0, trues = 0, falses = 0, errors = 0, unmutated_ok = 0;
+  long tab_checks = 0, tab_wide = 0, static_checks = 0, static_wide = 0;
   for (const Entry& e : corpus) {
     for (int k = 0; k <= mutants; ++k) {
       const std::string text = k == 0 ? e.text : mutate(e.text, rng);
@@ -182,13 +184,54 @@ int main(int argc, char** argv) {
       ++compiled;
       if (k == 0) ++unmutated_ok;
       if (!hm.user) continue;  // (no user invariant named: nothing to evaluate)
-      const std::string dev = tlcg::user_device_source(*hm.user);
+      const std::string dev = tlcg::user_device_source(*hm.user, hm.L);
       if (dev.find("tlcg_user_eval") == std::string::npos) {
         std::fprintf(stderr, "device source without tlcg_user_eval (case %s)\n", e.name.c_str());
         return 1;
       }
+      // the per-component outcome tables (component_code.h code_consts_user):
+      // the program on a code equals its value on the pattern of the code
+      // bits its fields take, unless that evaluation read past them (wide)
+      const uint32_t fm = tlcg::code_field_mask(hm.L, tlcg::user_fields(*hm.user, 0));
+      const int mb = hm.L.msg_sh + hm.L.N * hm.L.mw;
+      const tlcg::UserProg pruned = tlcg::user_prune_dead(*hm.user);
+      const bool reads_msgs = (tlcg::user_const_reads(*hm.user, 0) & 2u) != 0;
+      for (uint64_t s : states) {
+        const tlcg::CodeConsts kc = tlcg::code_consts(hm.L, tlcg::comp_msgs_init(hm.L, s));
+        const tlcg::lkey lk = (tlcg::lkey)(s >> mb);
+        const tlcg::ckey c = tlcg::code_encode(hm.L, lk);
+        if ((s >> mb) != (uint64_t)lk || tlcg::code_decode(hm.L, kc, c) != lk) continue;
+        const int direct = tlcg::eval_user_v(*hm.user, 0, tlcg::UVCode<uint64_t>{hm.L, kc, c});
+        const tlcg::UVTab<uint64_t> v{{hm.L, kc, tlcg::code_pdep(tlcg::code_pext(c, fm), fm)}};
+        const int tab = tlcg::eval_user_v(*hm.user, 0, v);
+        ++tab_checks;
+        if (v.wide) ++tab_wide;
+        else if (tab != direct) {
+          std::fprintf(stderr, "outcome table differs: case %s mutant %d state %llx: %d vs %d (fields %x)\n",
+                       e.name.c_str(), k, (unsigned long long)s, tab, direct, tlcg::user_fields(*hm.user, 0));
+          return 1;
+        }
+        // the host-made table of the state's class (Len, ledger content), for
+        // a program that reads no `messages` (the static tables)
+        if (!reads_msgs && kc.len <= (uint32_t)hm.L.N && tlcg::popcount32(fm) <= 5) {
+          const uint64_t st = tlcg::user_static_table(pruned, hm.L, 0, fm, (int)kc.len, (uint32_t)(kc.ledbits >> 1));
+          const int se = (int)((st >> (2 * tlcg::code_pext(c, fm))) & 3u);
+          ++static_checks;
+          if (se == 3) ++static_wide;
+          else if (se != direct) {
+            std::fprintf(stderr, "class table differs: case %s mutant %d state %llx: %d vs %d\n", e.name.c_str(), k,
+                         (unsigned long long)s, se, direct);
+            return 1;
+          }
+        }
+      }
       for (uint64_t s : states) {
         const int r = tlcg::eval_user<uint64_t>(hm.L, *hm.user, 0, s);
+        if (tlcg::eval_user<uint64_t>(hm.L, pruned, 0, s) != r) {
+          std::fprintf(stderr, "the pruned program differs: case %s mutant %d state %llx\n", e.name.c_str(), k,
+                       (unsigned long long)s);
+          return 1;
+        }
         ++evals;
         if (r == tlcg::EV_TRUE) ++trues;
         else if (r == tlcg::EV_FALSE) ++falses;
@@ -201,7 +244,9 @@ int main(int argc, char** argv) {
     }
   }
   std::printf("{\"entries\": %zu, \"unmutated_ok\": %ld, \"compiled\": %ld, \"refused\": %ld, \"states\": %zu, "
-              "\"evals\": %ld, \"true\": %ld, \"false\": %ld, \"error\": %ld}\n",
-              corpus.size(), unmutated_ok, compiled, refused, states.size(), evals, trues, falses, errors);
+              "\"evals\": %ld, \"true\": %ld, \"false\": %ld, \"error\": %ld, \"table_checks\": %ld, "
+              "\"table_wide\": %ld, \"static_checks\": %ld, \"static_wide\": %ld}\n",
+              corpus.size(), unmutated_ok, compiled, refused, states.size(), evals, trues, falses, errors, tab_checks,
+              tab_wide, static_checks, static_wide);
   return 0;
 }

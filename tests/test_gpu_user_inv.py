@@ -118,6 +118,31 @@ def test_user_invariant_on_chip(case):
     ck.close()
 
 
+@pytest.mark.parametrize("utab", ["0", "dyn", "slow"])
+@pytest.mark.parametrize("case", ["U_LedgerCount", "U_all_hold", "U_ContextLedgerError", "U_mixed_user_first",
+                                  "U_noretain_LatestIsLast", "U_C5_ContextBound"])
+def test_user_invariant_outcome_tables(case, utab, monkeypatch):
+    """the outcome tables (component_code.h code_consts_user) against the
+    programs: no tables (TLCG_UTAB=0), tables filled per component only
+    (dyn), and every entry left to the kernel's fallback evaluation (slow)
+    give the same verdict, counts, trace and stop counters as the default
+    (host-made class tables + per-component ones) -- the golden fixture"""
+    monkeypatch.setenv("TLCG_UTAB", utab)
+    m = model(case)
+    want = GOLD[case]["result"]
+    ck = tlcgpu.Checker(m)
+    r = ck.run()
+    assert r.status == want["result"], (case, utab, r.status)
+    if want["result"] == "ok":
+        assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                                 want["levels"])
+    else:
+        assert r.depth == want["depth"] and (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+        assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
+        assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"])
+    ck.close()
+
+
 @pytest.mark.parametrize("case", ["U_LedgerCount", "U_all_hold", "U_ContextLedgerError", "U_mixed_user_first",
                                   "U_C5_ContextBound"])
 def test_user_invariant_tree_closed_mode(case):

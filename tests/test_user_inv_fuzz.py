@@ -63,6 +63,8 @@ def test_user_inv_compiler_under_sanitizers(fuzz_bin, tmp_path, seed):
     assert res["entries"] == n and res["unmutated_ok"] == n  # every fixture compiles as written
     assert res["compiled"] > n and res["refused"] > 0 and res["evals"] > 0
     assert res["true"] + res["false"] + res["error"] == res["evals"]
+    # the outcome tables agree with the programs (component_code.h code_consts_user)
+    assert res["table_checks"] > 0 and res["static_checks"] > 0
 
 
 REF = "/root/reference"
