@@ -76,7 +76,6 @@ BYTES_PER_STATE_WORD = 8
 
 # the newest round's profile of each kind (profiles/rNN_*), measured on the same kernels
 PMC_PROFILE = "pmc_k_expand.json"
-PMC_COMPONENT_PROFILE = "pmc_component.json"
 COMPONENT_BYTES_PER_STATE = 4  # the code pass writes one 32-bit record per state (component.h comp_record)
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
 # algorithmic HBM bytes per distinct state of the BFS path (read
@@ -91,7 +90,10 @@ CUS, SIMDS, CLOCK_HZ = 256, 4, 2.4e9
 
 
 def component_kernel_name(jit):
-    """the first-pass component kernel tlcg_stats.jit_used names (bit 0 hipRTC, bit 1 codes)"""
+    """the first-pass component kernel tlcg_stats.jit_used names (bit 0 hipRTC, bit 1 codes,
+    bit 3 one walk of the code graph per wavefront)"""
+    if jit & 8:
+        return "tlcg_componentw_64 (hipRTC-specialized, component codes, one code-graph walk per wavefront)"
     if jit & 1:
         return "tlcg_componentc_64 (hipRTC-specialized, component codes)" if jit & 2 else \
             "tlcg_component_64 (hipRTC-specialized)"
@@ -462,13 +464,21 @@ def main():
                              "(16-B records) + ncclAllReduce per level, RCCL over xGMI")
 
     open_model = bool(cfg.get("producer"))
-    global_run = None
+    global_run = perlane_run = None
     if open_model and distributed:
         # the component tree split by subtrees (no exchange), or the level loop's exchange if it hands over
         main_run = time_exchange(0)
     else:
         main_run = time_engine("auto")
         global_run = time_engine("global")  # the HBM-FPSet engine beside the on-chip one
+        if main_run["engine"] == "component" and main_run["jit"] & 8:
+            # the component engine's per-lane kernel (component_body.h: every lane
+            # its own FIFO and FPSet) beside the one walk per wavefront
+            os.environ["TLCG_COMP_WAVE"] = "0"
+            try:
+                perlane_run = time_engine("auto")
+            finally:
+                os.environ.pop("TLCG_COMP_WAVE", None)
     distinct, generated = cfg["distinct"], cfg["generated"]
     # (a producer-modelled cfg has one initial state; its Terminating stutters
     # are not counted out of the probes, so its bytes/state is an upper bound)
@@ -511,48 +521,38 @@ def main():
                 frac=round(bound_ms / r["expand_ms"], 3), source=MICRO_PROFILE)
         return rf
 
+    def survey_equivalent(r):
+        """SURVEY 8(d)'s 34.7 B per distinct state (the HBM-FPSet design's bytes)
+        at this run's speed: a notional rate, not the kernel's traffic"""
+        gbs = SURVEY_BYTES_PER_DISTINCT * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
+        return dict(bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4),
+                    note="notional: the on-chip engines keep their FPSet and FIFO in LDS and never move these bytes")
+
     def roofline_component(r):
-        # SURVEY 8(d)'s per-unit figure x the distinct states of one launch; the
-        # kernel itself only writes a 4-B record per state (the FPSet and queue
-        # stay on chip; the 32-bit cascade passes, none on G9, write 16 B)
-        bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
-        achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
-        written = COMPONENT_BYTES_PER_STATE * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
+        # the kernel's own algorithmic HBM bytes: one 4-B record written per
+        # distinct state (comp_record; its FIFO and FPSet stay in LDS, the
+        # components' constants come from the initial-state index; the 32-bit
+        # cascade passes, none on G9, write 16 B); SURVEY 8(d)'s 34.7 B/state
+        # (the HBM-FPSet design's) beside it as survey_equivalent
+        kt = r["expand_ms"] * 1e-3
+        achieved = COMPONENT_BYTES_PER_STATE * distinct / world / kt / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
                   kernel=component_kernel_name(r["jit"]),
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
-                  kernel_bytes_per_distinct=COMPONENT_BYTES_PER_STATE,
-                  kernel_written_gbs=round(written, 1))
-        kt = r["expand_ms"] * 1e-3
-        new = pmc_fields(f"component_{args.config}", rf["kernel"], kt, distinct) if world == 1 else None
+                  bytes_per_distinct=COMPONENT_BYTES_PER_STATE,
+                  bytes_basis="the kernel's HBM bytes per distinct state: its 4-B store record (DESIGN 4)",
+                  survey_equivalent=survey_equivalent(r))
+        # (each kernel priced with its own profile: component_<cfg> = the one walk per
+        # wavefront, component_perlane_<cfg> = component_body.h's lanes)
+        new = None
+        if world == 1:
+            for prof in ([f"component_{args.config}"] if r["jit"] & 8 else
+                         [f"component_perlane_{args.config}", f"component_{args.config}"]):
+                new = new or pmc_fields(prof, rf["kernel"], kt, distinct)
         if new:
             rf.update(new)
-            return rf
-        pmc = load_profile(PMC_COMPONENT_PROFILE)
-        # (the counters are of one kernel variant: used only for that variant)
-        if pmc and args.config == "g9" and world == 1 and pmc["kernel"].split()[0] == rf["kernel"].split()[0]:
-            c = pmc["counters"]
-            kt = r["expand_ms"] * 1e-3
-            rf["traffic"] = round(pmc["hbm_bytes_per_step"] / kt / 1e9, 1)
-            rf["traffic_bytes_per_launch"] = round(pmc["hbm_bytes_per_step"])
-            rf["traffic_source"] = pmc["_file"]
-            # issue bound: each port's busy time at full rate / the kernel's time
-            t_valu = c["SQ_INSTS_VALU"] * 2 / (CUS * SIMDS * CLOCK_HZ)
-            t_salu = c["SQ_INSTS_SALU"] / (CUS * CLOCK_HZ)
-            t_lds = c["SQ_LDS_IDX_ACTIVE"] / (CUS * CLOCK_HZ)
-            t_sum = (c["SQ_INSTS_VALU"] + c["SQ_INSTS_SALU"] + c["SQ_INSTS_LDS"]) / (CUS * SIMDS * CLOCK_HZ)
-            rf["issue"] = dict(
-                frac=round(max(t_valu, t_salu, t_lds) / kt, 3),
-                frac_all_ports_one_issue=round(t_sum / kt, 3),
-                valu_ms=round(t_valu * 1e3, 3), salu_ms=round(t_salu * 1e3, 3), lds_ms=round(t_lds * 1e3, 3),
-                valu_wave_insts_per_state=round(c["SQ_INSTS_VALU"] / distinct, 3),
-                salu_wave_insts_per_state=round(c["SQ_INSTS_SALU"] / distinct, 3),
-                lds_wave_insts_per_state=round(c["SQ_INSTS_LDS"] / distinct, 3),
-                wave_issue_frac=round(pmc["wave_issue_frac"], 3),
-                formula="frac = max(VALU x 2 cyc / (256 CU x 4 SIMD), SALU x 1 cyc / 256 CU, "
-                        "SQ_LDS_IDX_ACTIVE / 256 CU) / 2.4 GHz / kernel time (DESIGN 4)")
+            rf["traffic_over_algorithmic"] = round(new["traffic_bytes_per_step"] / (COMPONENT_BYTES_PER_STATE * distinct), 3)
         return rf
 
     def roofline_tree(r):
@@ -561,9 +561,8 @@ def main():
         # modelled, plus a depth byte the next layer reads with the parent
         # state, 9 B per entry) or, closed, the 4-B component code the host
         # decodes (tree_body.h TLCG_TREE_CODE_STORE); its FPSets stay in LDS
-        bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
-        achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
         per_state = BYTES_PER_STATE_WORD * (words + 1) + 1 if open_model else 4 + BYTES_PER_STATE_WORD
+        achieved = per_state * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
         if open_model:
             kern = ("tlcg_tree_384 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<384, 512, 4> (") + \
                 "component tree, 4 components per wavefront)"
@@ -573,8 +572,10 @@ def main():
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kern,
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, kernel_bytes_per_distinct=per_state,
-                  kernel_written_gbs=round(per_state * distinct / world / (r["expand_ms"] * 1e-3) / 1e9, 1))
+                  bytes_per_distinct=per_state,
+                  bytes_basis="the kernel's HBM bytes per distinct state: the stored state or code and its parent "
+                              "reference (DESIGN 4)",
+                  survey_equivalent=survey_equivalent(r))
         new = pmc_fields(f"tree_{args.config}", kern, r["expand_ms"] * 1e-3, distinct) if world == 1 else None
         if new:
             rf.update(new)
@@ -623,6 +624,8 @@ def main():
             line["config"]["user_invariants"] = {n: USER_DEFS[n] for n in user_invariants(args.config)}
         if global_run:
             line["engines"]["global_hbm_fpset"] = summary(global_run)
+        if perlane_run:
+            line["engines"]["component_per_lane"] = summary(perlane_run)
         if distributed:
             line["dist_backend"] = args.dist_backend
             line["rccl_ranks"] = preflight["rccl_ranks"] if preflight else None

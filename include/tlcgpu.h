@@ -167,7 +167,9 @@ typedef struct tlcg_stats {
   uint64_t jit_used;         /* bit 0: the layout-specialized (hipRTC) component kernels ran;
                                 bit 1: the component engine ran component codes (16-bit lanes);
                                 bit 2: user invariants: the global engine's check is device code
-                                (hipRTC, tlcg_user_check), not the interpreter */
+                                (hipRTC, tlcg_user_check), not the interpreter;
+                                bit 3: the code pass walked each code graph once per wavefront
+                                for its components (tlcg_componentw_64, component_wave.h) */
   uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
   uint64_t fpset_host_states; /* states held by the host FPSet tier (tlcg_opts.fpset_spill) */
   uint64_t transport;        /* multi-rank runs: 1 host threads + device copies, 2 RCCL; 0 one context */

@@ -74,6 +74,10 @@ std::string program_source(const Layout& L, const std::string& user, bool check_
              "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ", " + od + ", " + code +
              ">(a, kL); }\n";
       }
+  // the first pass with one walk of the code graph per wave (component_wave.h)
+  for (const char* od : {"false", "true"})
+    s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_componentw") + (od[0] == 't' ? "od" : "") +
+         "_64(tlcg::CompArgs a) { tlcg::component_wave_body<64, " + od + ">(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_384(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_1024(tlcg::TreeArgs a) "
@@ -232,6 +236,12 @@ bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStr
 
 bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user) {
   if (!load_module(L, device, user, false, &out->module, &out->cached, &out->compile_s, err)) return false;
+  out->wave_m = user.empty() ? WAVE_M : WAVE_M_USER;  // (component_wave.h TLCG_WAVE_M)
+  if (hipModuleGetFunction(&out->wave[0], out->module, "tlcg_componentw_64") != hipSuccess ||
+      hipModuleGetFunction(&out->wave[1], out->module, "tlcg_componentwod_64") != hipSuccess) {
+    *err = "hipModuleGetFunction tlcg_componentw_64";
+    return false;
+  }
   const char* names[4] = {"32", "64", "128", "255"};
   for (int i = 0; i < 4; ++i)
     for (int od = 0; od < 2; ++od) {
@@ -263,12 +273,14 @@ void jit_release(JitKernels* k) {
   if (k) *k = JitKernels();
 }
 
-bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream) {
+bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream, bool wave) {
   if (!a.n_comp) return true;
   const int i = K == 32 ? 0 : K == 64 ? 1 : K == 128 ? 2 : 3;
   hipFunction_t f = a.outdeg ? k.component_od[i] : k.component[i];
   if (code && i < 2) f = a.outdeg ? k.code_od[i] : k.code[i];
-  const uint64_t batches = (a.n_comp + 63) / 64;
+  const bool w = wave && code && K == 64;
+  if (w) f = a.outdeg ? k.wave[1] : k.wave[0];
+  const uint64_t batches = w ? (a.n_comp + 64 * (u64)k.wave_m - 1) / (64 * (u64)k.wave_m) : (a.n_comp + 63) / 64;
   const unsigned grid = (unsigned)(batches < comp_grid_cap() ? batches : comp_grid_cap());
   CompArgs copy = a;
   void* args[] = {&copy};

@@ -19,6 +19,8 @@ struct JitKernels {
   hipFunction_t component_od[4] = {nullptr, nullptr, nullptr, nullptr};  // the same, counting outdegrees
   hipFunction_t code[2] = {nullptr, nullptr};     // component codes (component_code.h), K = 32, 64
   hipFunction_t code_od[2] = {nullptr, nullptr};
+  hipFunction_t wave[2] = {nullptr, nullptr};     // codes, K = 64, one walk per wave (component_wave.h); outdegrees
+  int wave_m = WAVE_M;                            // its components per lane (the grid)
   hipFunction_t tree[4] = {nullptr, nullptr, nullptr, nullptr};  // component tree: 384 x 4 groups, 1024 x 1;
                                                                  // closed mode: 640 x 4, 2048 x 1
   double compile_s = 0;  // 0 when loaded from the cache
@@ -35,7 +37,9 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
                  const std::string& user = "", bool check_only = false);
 void jit_release(JitKernels* k);
-bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream);
+// (wave: the first pass's kernel with one walk of the code graph per wave, component_wave.h)
+bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream,
+                          bool wave = false);
 // the global engine's user-invariant check (kernels.h user_check_body) as
 // device code: a module of its own, so a global-engine check does not wait
 // for the on-chip engines' kernels to compile

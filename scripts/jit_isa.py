@@ -24,6 +24,12 @@ n = tlcgpu.load_library().tlcg_jit_selftest(C.byref(cm), b"gfx950", err, 8192)
 if n < 0:
     raise SystemExit(err.value.decode())
 opts = os.environ.get("TLCG_JIT_OPTS", "-mllvm -amdgpu-sched-strategy=max-ilp").split()
+# the dumped source holds the headers inline; its own #include lines resolve to empty stubs
+import re  # noqa: E402
+stub = out + "_inc"
+os.makedirs(stub, exist_ok=True)
+for h in set(re.findall(r'#include "([^"]+)"', open(out + ".hip").read())):
+    open(os.path.join(stub, h), "w").close()
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-x", "hip", "--cuda-device-only",
-                "-S", "-o", out + ".s", out + ".hip"] + opts, check=True)
+                "-S", "-I" + stub, "-o", out + ".s", out + ".hip"] + opts, check=True)
 print(out + ".s")
