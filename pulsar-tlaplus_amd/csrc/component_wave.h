@@ -167,6 +167,9 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
     };
     int head = 0, tail = 1, level = 0, lvl_start = 0, lvl_end = 1;  // the walk's (scalar)
     unsigned lvgen = 0;
+    // the records of batches b0 .. b0+M-1 (range-checked raw buffer stores)
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint32_t*>(a.store) + b0 * (u64)K * 64, (short)0, M * K * 64 * 4, 0x00020000);
     uint32_t cur = vcopy(cu0);  // the walk's data: vector registers, the same in every lane
     while (any_run()) {
       const uint32_t s = cur;
@@ -197,12 +200,15 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
         h[sl] = (uint8_t)(tail + 1);
         q[tail] = (uint16_t)key;
         const uint32_t rec = comp_record(key, head, act_id);
+        // each running component's record and invariants, with no branch per
+        // component: a component out of the walk stores out of the buffer's
+        // range (the hardware drops the store) and its outcome is masked
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          if (run[m]) {
-            reinterpret_cast<uint32_t*>(a.store)[((b0 + m) * (u64)K + (u64)tail) * 64 + (u64)lane] = rec;
-            evk[m] = check_invariants_cbt(L, ccon[m], key) + 1;
-          }
+          const int off = run[m] ? (int)(((unsigned)m * K + (unsigned)tail) * 64u + (unsigned)lane) * 4 : 0x7fffffff;
+          __builtin_amdgcn_raw_buffer_store_b32(rec, rsrc, off, 0, 0);
+          const int e = check_invariants_cbt(L, ccon[m], key) + 1;
+          evk[m] = run[m] ? e : 0;
         }
         ++tail;
         __syncthreads();  // (the shared queue and table written)
@@ -222,6 +228,10 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       // each component's events: an action error, a deadlock (both the
       // walk's), an invariant of an inserted successor (its own); the rare branch
       const bool walk_ev = (r == 2) | (nsucc == 0 && L.check_deadlock);
+      bool any_ev = false;
+#pragma unroll
+      for (int m = 0; m < M; ++m) any_ev = any_ev | (run[m] & (walk_ev | (ev1[m] != 0) | (ev2[m] != 0)));
+      if (any_ev) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         if (run[m] && (walk_ev | (ev1[m] != 0) | (ev2[m] != 0))) {
@@ -246,6 +256,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
           stop[m] = stop[m] || k != NO_EVENT;
         }
       }
+      }
       ++head;
       cur = head < tail0 ? nxt : first_new;  // position head was filled by this expansion
       const bool done = head >= tail;        // the component ran out (every component of the walk)
@@ -267,6 +278,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       // the cascade, too deep or no room for the next expansion's two
       // successors (component_body.h's order of these tests)
       int nq = 0;
+      if (ended || done || tail > K - 2)  // (the walk's conditions: most expansions skip this)
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const bool quit = run[m] && !deep && ((ended && stop[m]) || done);
