@@ -69,8 +69,17 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
   // (wave w walks batches w*M .. w*M+M-1; component (batch bm, lane) as in component_body.h)
   for (u64 b0 = (u64)blockIdx.x * M; b0 * 64 < a.n_comp; b0 += (u64)gridDim.x * M) {
     for (int i = lane; i < T; i += 64) h[i] = 0;
-    u64 idx0[M];
+    // component m's initial-state index (kept in no register: recomputed)
+    auto idx0 = [&](int m) -> u64 {
+      const u64 ci = (b0 + m) * 64 + (u64)lane;
+      return ci < a.n_comp ? (a.list ? a.list[ci] : a.comp0 + ci) & ((1ull << 40) - 1) : 0;  // (a first pass)
+    };
     CodeConsts ccon[M];
+#ifndef TLCG_USER_INV
+    // past the start, a component of the walk keeps only the flags of its
+    // constants (its Len is the walk's): one register instead of a CodeConsts
+    uint32_t kf[M];
+#endif
     ckey c0[M];
     bool code_ok[M];
     u64 okm = 0;
@@ -78,8 +87,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
     for (int m = 0; m < M; ++m) {
       const u64 ci = (b0 + m) * 64 + (u64)lane;
       const bool act = ci < a.n_comp;
-      idx0[m] = act ? (a.list ? a.list[ci] : a.comp0 + ci) & ((1ull << 40) - 1) : 0;  // (a first pass)
-      const u64 s0 = init_state(L, idx0[m]);
+      const u64 s0 = init_state(L, idx0(m));
       ccon[m] = code_consts(L, comp_msgs_init(L, s0));
 #ifdef TLCG_USER_INV
       code_consts_user(L, ccon[m]);  // the user invariants' outcome tables of this component
@@ -87,6 +95,10 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       const lkey k0 = (lkey)(s0 >> mb);
       c0[m] = code_encode(L, k0);
       code_ok[m] = act && code_decode(L, ccon[m], c0[m]) == k0;
+#ifndef TLCG_USER_INV
+      kf[m] = (uint32_t)(ccon[m].msgs_ok != 0) | (uint32_t)(ccon[m].hz_live != 0) << 1 |
+              (uint32_t)(ccon[m].hz_false != 0) << 2 | (uint32_t)(ccon[m].dn0 != 0) << 3 | (uint32_t)(ccon[m].dn1 != 0) << 4;
+#endif
       okm |= __ballot(code_ok[m]);
     }
     // the walk's leader: the first component of batch 0..M-1 with a code
@@ -110,18 +122,33 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
     const ckey cu0 = (ckey)__builtin_amdgcn_readlane((int)lc, leader);
     const uint32_t lenu = (uint32_t)__builtin_amdgcn_readlane((int)ll, leader);
     // the components of the walk; the others (another code graph, or no code) go on to the cascade
+    // (an event key goes to `ev` when found: a component that later leaves for
+    // the cascade finds the same key again there)
     bool run[M], stop[M];
-    u64 lev[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const bool act = (b0 + m) * 64 + (u64)lane < a.n_comp;
       run[m] = code_ok[m] && c0[m] == cu0 && ccon[m].len == lenu;
       stop[m] = false;
-      lev[m] = NO_EVENT;
-      if (act && !run[m]) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0[m];
+      if (act && !run[m]) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0(m);
     }
     CodeConsts cu{};  // the transitions read Len only
     cu.len = lenu;
+    // component m's constants for its invariants (a component of the walk has the walk's Len)
+    auto kc = [&](int m) -> CodeConsts {
+#ifdef TLCG_USER_INV
+      return ccon[m];
+#else
+      CodeConsts k{};
+      k.len = lenu;
+      k.msgs_ok = kf[m] & 1;
+      k.hz_live = (kf[m] >> 1) & 1;
+      k.hz_false = (kf[m] >> 2) & 1;
+      k.dn0 = (kf[m] >> 3) & 1;
+      k.dn1 = (kf[m] >> 4) & 1;
+      return k;
+#endif
+    };
     __syncthreads();  // (the cleared table)
     if (!okm) continue;
     if (lane == 0) {
@@ -136,13 +163,12 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       uint32_t* const recb = reinterpret_cast<uint32_t*>(a.store) + (b0 + m) * (u64)K * 64;
       if (run[m]) {
         recb[lane] = comp_record(cu0, 0, 0);
-        const int c = check_invariants_direct(L, ccon[m], cu0);
+        const int c = check_invariants_direct(L, kc(m), cu0);
         if (c >= 0) {  // an initial state violates: level 0 is complete, nothing is expanded
-          lev[m] = make_comp_event(0, idx0[m], 0, 0, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1);
+          ev = min(ev, (unsigned long long)make_comp_event(0, idx0(m), 0, 0, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
           run[m] = false;
           gen += 1;
           dist += 1;
-          ev = min(ev, (unsigned long long)lev[m]);
           ++n0;
         }
       }
@@ -207,7 +233,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
         for (int m = 0; m < M; ++m) {
           const int off = run[m] ? (int)(((unsigned)m * K + (unsigned)tail) * 64u + (unsigned)lane) * 4 : 0x7fffffff;
           __builtin_amdgcn_raw_buffer_store_b32(rec, rsrc, off, 0, 0);
-          const int e = check_invariants_cbt(L, ccon[m], key) + 1;
+          const int e = check_invariants_cbt(L, kc(m), key) + 1;
           evk[m] = run[m] ? e : 0;
         }
         ++tail;
@@ -238,21 +264,21 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
 #pragma nounroll
           for (int i = 0; i < 2; ++i) {  // an outcome table left it to the programs
             if ((i ? ev2[m] : ev1[m]) == INV_UNKNOWN + 1) {
-              const int e = check_invariants_direct(L, ccon[m], i ? t2 : t) + 1;
+              const int e = check_invariants_direct(L, kc(m), i ? t2 : t) + 1;
               if (i) ev2[m] = e;
               else ev1[m] = e;
             }
           }
-          u64 k = r == 2 ? make_comp_event(level + 1, idx0[m], head, action, EVK_ACTION_ERROR, action)
-                  : nsucc == 0 && L.check_deadlock ? make_comp_event(level + 1, idx0[m], head, 15, EVK_DEADLOCK, 0)
+          u64 k = r == 2 ? make_comp_event(level + 1, idx0(m), head, action, EVK_ACTION_ERROR, action)
+                  : nsucc == 0 && L.check_deadlock ? make_comp_event(level + 1, idx0(m), head, 15, EVK_DEADLOCK, 0)
                                                    : NO_EVENT;
           if (ev1[m])
-            k = min(k, make_comp_event(level + 1, idx0[m], head, action, ((ev1[m] - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
+            k = min(k, make_comp_event(level + 1, idx0(m), head, action, ((ev1[m] - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
                                        (ev1[m] - 1) >> 1));
           if (ev2[m])
-            k = min(k, make_comp_event(level + 1, idx0[m], head, ACT_CRASH,
+            k = min(k, make_comp_event(level + 1, idx0(m), head, ACT_CRASH,
                                        ((ev2[m] - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION, (ev2[m] - 1) >> 1));
-          lev[m] = min(lev[m], k);
+          ev = min(ev, (unsigned long long)k);
           stop[m] = stop[m] || k != NO_EVENT;
         }
       }
@@ -283,7 +309,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       for (int m = 0; m < M; ++m) {
         const bool quit = run[m] && !deep && ((ended && stop[m]) || done);
         const bool ovf = run[m] && !quit && (deep || tail > K - 2);
-        if (ovf) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0[m] | ((u64)level << 40);  // levels < `level` counted
+        if (ovf) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0(m) | ((u64)level << 40);  // levels < `level` counted
         if (quit) {
           // the last level [lvl_start, tail) was discovered, not expanded
           gen += lgen;
@@ -293,7 +319,6 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
             od1 += (ocnt >> 10) & 1023;
             od2 += ocnt >> 20;
           }
-          ev = min(ev, (unsigned long long)lev[m]);
           ++nq;
         }
         run[m] = run[m] && !ovf && !quit;

@@ -34,9 +34,13 @@ std::string layout_literal(const Layout& L) {
   return o.str();
 }
 
-// check_only: the user-invariant check kernel alone (tlcg_user_check, the
-// global engine's; compiles in a fraction of the whole module's time)
-std::string program_source(const Layout& L, const std::string& user, bool check_only = false) {
+// part: 0 the on-chip engines' kernels; 1 (JIT_CHECK) the user-invariant
+// check kernel alone (tlcg_user_check, the global engine's; compiles in a
+// fraction of the whole module's time); 2 (JIT_WAVE) the component code
+// pass's one-walk-per-wavefront kernels, a module of their own so that they
+// are scheduled with options of their own (jit_opts)
+std::string program_source(const Layout& L, const std::string& user, int part = JIT_MAIN) {
+  const bool check_only = part == JIT_CHECK;
   std::string s = "typedef unsigned char uint8_t; typedef unsigned short uint16_t; typedef unsigned int uint32_t; typedef int int32_t;\n"
                   "typedef unsigned long uint64_t; typedef long int64_t;\n";
   // user invariants: the headers' check functions call tlcg_user_eval (model.h)
@@ -64,6 +68,13 @@ std::string program_source(const Layout& L, const std::string& user, bool check_
          "{ tlcg::user_check_body<" + w + ">(a, kL); }\n";
     return s;
   }
+  if (part == JIT_WAVE) {
+    // the first pass with one walk of the code graph per wave (component_wave.h)
+    for (const char* od : {"false", "true"})
+      s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_componentw") +
+           (od[0] == 't' ? "od" : "") + "_64(tlcg::CompArgs a) { tlcg::component_wave_body<64, " + od + ">(a, kL); }\n";
+    return s;
+  }
   for (int K : {32, 64, 128, 255})
     for (const char* od : {"false", "true"})
       for (const char* code : {"false", "true"}) {
@@ -74,10 +85,6 @@ std::string program_source(const Layout& L, const std::string& user, bool check_
              "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ", " + od + ", " + code +
              ">(a, kL); }\n";
       }
-  // the first pass with one walk of the code graph per wave (component_wave.h)
-  for (const char* od : {"false", "true"})
-    s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_componentw") + (od[0] == 't' ? "od" : "") +
-         "_64(tlcg::CompArgs a) { tlcg::component_wave_body<64, " + od + ">(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_384(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_1024(tlcg::TreeArgs a) "
@@ -100,9 +107,11 @@ std::string program_source(const Layout& L, const std::string& user, bool check_
 // 4.79; interleaved on one box, profiles/r04_probe_sched2.jsonl).  The
 // precompiled global-engine kernels showed no steady gain from it (G9 88 / 95
 // vs 81 / 99 ms, M8 16.9 vs 17.2; r04_probe_sched_global.jsonl): not used there
-std::string jit_opts() {
-  const char* e = std::getenv("TLCG_JIT_OPTS");
-  return e ? e : "-mllvm -amdgpu-sched-strategy=max-ilp";
+// The wave kernels' module (JIT_WAVE) takes the default machine scheduler
+// (TLCG_JIT_OPTS_WAVE): max-ILP measured slower there (G9 1.39-1.41 vs 1.28 ms).
+std::string jit_opts(int part) {
+  const char* e = std::getenv(part == JIT_WAVE ? "TLCG_JIT_OPTS_WAVE" : "TLCG_JIT_OPTS");
+  return e ? e : part == JIT_WAVE ? "" : "-mllvm -amdgpu-sched-strategy=max-ilp";
 }
 
 uint64_t fnv1a(const std::string& s) {
@@ -126,10 +135,11 @@ bool read_all(const std::string& p, std::vector<char>* out) {
 }  // namespace
 
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
-                 const std::string& user, bool check_only) {
-  const std::string src = program_source(L, user, check_only);
+                 const std::string& user, int part) {
+  const std::string src = program_source(L, user, part);
   const char* dump_env = std::getenv("TLCG_JIT_DUMP");  // diagnostics: the generated source and code object
-  const std::string dump = dump_env ? std::string(dump_env) + (check_only ? ".check" : "") : "";
+  const std::string dump =
+      dump_env ? std::string(dump_env) + (part == JIT_CHECK ? ".check" : part == JIT_WAVE ? ".wave" : "") : "";
   if (dump_env) {
     std::ofstream f(dump);
     f << src;
@@ -141,7 +151,7 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
   }
   const std::string a = "--offload-arch=" + arch;
   std::vector<std::string> extra;
-  std::istringstream in(jit_opts());
+  std::istringstream in(jit_opts(part));
   for (std::string w; in >> w;) extra.push_back(w);
   std::vector<const char*> opts = {a.c_str(), "-O3", "-std=c++20"};
   for (const std::string& w : extra) opts.push_back(w.c_str());
@@ -169,9 +179,9 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
 
 namespace {
 
-// the code object of program_source(L, user, check_only) for `device`: from the
+// the code object of program_source(L, user, part) for `device`: from the
 // cache, else compiled and cached; loaded into *module
-bool load_module(const Layout& L, int device, const std::string& user, bool check_only, hipModule_t* module,
+bool load_module(const Layout& L, int device, const std::string& user, int part, hipModule_t* module,
                  bool* cached, double* compile_s, std::string* err) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
@@ -180,16 +190,16 @@ bool load_module(const Layout& L, int device, const std::string& user, bool chec
   }
   std::string arch = prop.gcnArchName;
   arch = arch.substr(0, arch.find(':'));
-  const std::string src = program_source(L, user, check_only);
+  const std::string src = program_source(L, user, part);
   char key[64];
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2" + jit_opts()));
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|" + arch + "|v2" + jit_opts(part)));
   const std::string dir = cache_dir();
   const std::string path = dir + "/" + key + "-" + arch + ".co";
   std::vector<char> code;
   *cached = read_all(path, &code);
   if (!*cached) {
     auto t0 = std::chrono::steady_clock::now();
-    if (!jit_compile(L, arch, &code, err, user, check_only)) return false;
+    if (!jit_compile(L, arch, &code, err, user, part)) return false;
     *compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     mkdir(dir.c_str(), 0777);
     const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
@@ -211,7 +221,7 @@ bool load_module(const Layout& L, int device, const std::string& user, bool chec
 bool jit_build_user_check(const Layout& L, int device, const std::string& user, JitUserCheck* out, std::string* err) {
   double cs = 0;
   bool cached = false;
-  if (!load_module(L, device, user, true, &out->module, &cached, &cs, err)) return false;
+  if (!load_module(L, device, user, JIT_CHECK, &out->module, &cached, &cs, err)) return false;
   out->compile_s = cs;
   if (hipModuleGetFunction(&out->fn, out->module, "tlcg_user_check") != hipSuccess) {
     *err = "hipModuleGetFunction tlcg_user_check";
@@ -235,10 +245,14 @@ bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStr
 }
 
 bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user) {
-  if (!load_module(L, device, user, false, &out->module, &out->cached, &out->compile_s, err)) return false;
+  if (!load_module(L, device, user, JIT_MAIN, &out->module, &out->cached, &out->compile_s, err)) return false;
+  bool wcached = false;
+  double wcs = 0;
+  if (!load_module(L, device, user, JIT_WAVE, &out->wave_module, &wcached, &wcs, err)) return false;
+  out->compile_s += wcs;
   out->wave_m = user.empty() ? WAVE_M : WAVE_M_USER;  // (component_wave.h TLCG_WAVE_M)
-  if (hipModuleGetFunction(&out->wave[0], out->module, "tlcg_componentw_64") != hipSuccess ||
-      hipModuleGetFunction(&out->wave[1], out->module, "tlcg_componentwod_64") != hipSuccess) {
+  if (hipModuleGetFunction(&out->wave[0], out->wave_module, "tlcg_componentw_64") != hipSuccess ||
+      hipModuleGetFunction(&out->wave[1], out->wave_module, "tlcg_componentwod_64") != hipSuccess) {
     *err = "hipModuleGetFunction tlcg_componentw_64";
     return false;
   }
@@ -270,6 +284,7 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
 
 void jit_release(JitKernels* k) {
   if (k && k->module) hipModuleUnload(k->module);
+  if (k && k->wave_module) hipModuleUnload(k->wave_module);
   if (k) *k = JitKernels();
 }
 

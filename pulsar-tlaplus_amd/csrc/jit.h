@@ -13,8 +13,12 @@
 
 namespace tlcg {
 
+// the parts of the specialized source (jit.cpp program_source): one module each
+enum JitPart { JIT_MAIN = 0, JIT_CHECK = 1, JIT_WAVE = 2 };
+
 struct JitKernels {
   hipModule_t module = nullptr;
+  hipModule_t wave_module = nullptr;  // JIT_WAVE
   hipFunction_t component[4] = {nullptr, nullptr, nullptr, nullptr};     // K = 32, 64, 128, 255
   hipFunction_t component_od[4] = {nullptr, nullptr, nullptr, nullptr};  // the same, counting outdegrees
   hipFunction_t code[2] = {nullptr, nullptr};     // component codes (component_code.h), K = 32, 64
@@ -33,9 +37,9 @@ struct JitKernels {
 // which the kernels then evaluate in the cfg's order with the spec's own.
 bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user = "");
 // compile only (no device needed): the code object for `arch`
-// (check_only: the user-check kernel alone, jit_build_user_check)
+// (part: JitPart -- JIT_CHECK the user-check kernel alone, jit_build_user_check; JIT_WAVE the wave kernels)
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
-                 const std::string& user = "", bool check_only = false);
+                 const std::string& user = "", int part = JIT_MAIN);
 void jit_release(JitKernels* k);
 // (wave: the first pass's kernel with one walk of the code graph per wave, component_wave.h)
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream,

@@ -33,3 +33,10 @@ for h in set(re.findall(r'#include "([^"]+)"', open(out + ".hip").read())):
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-x", "hip", "--cuda-device-only",
                 "-S", "-I" + stub, "-o", out + ".s", out + ".hip"] + opts, check=True)
 print(out + ".s")
+# the wave kernels' module (jit.cpp JIT_WAVE: the default scheduler unless TLCG_JIT_OPTS_WAVE)
+if os.path.exists(out + ".hip.wave"):
+    wopts = os.environ.get("TLCG_JIT_OPTS_WAVE", "").split()
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-x", "hip",
+                    "--cuda-device-only", "-S", "-I" + stub, "-x", "hip", "-o", out + ".wave.s",
+                    out + ".hip.wave"] + wopts, check=True)
+    print(out + ".wave.s")
