@@ -330,6 +330,7 @@ class LocalTransport;
 
 struct LocalBoard {
   int n = 0;
+  bool pull = false;  // every rank on one device (and TLCG_PULL != 0): absorbs read the outboxes in place
   std::vector<tlcg_ctx*> ctxs;
   std::vector<uint64_t> rows;               // n x (n + 1)
   std::vector<std::vector<uint64_t>> red;   // one vector per rank
@@ -398,6 +399,21 @@ class LocalTransport : public Transport {
     return ok;
   }
 
+  bool can_pull() const override { return b_->pull; }
+  void pull_sources(tlcg_ctx*, const uint64_t* recv, std::vector<const uint64_t*>* p,
+                    std::vector<uint64_t>* k) override {
+    p->clear();
+    k->clear();
+    for (int s = 0; s < b_->n; ++s) {
+      if (s == r_ || !recv[s]) continue;
+      void* q = nullptr;
+      tlcg_outbox(b_->ctxs[(size_t)s], r_, &q, nullptr);
+      p->push_back(static_cast<const uint64_t*>(q));
+      k->push_back(recv[s]);
+    }
+  }
+  void pulled() override { b_->barrier(); }
+
   bool allreduce(uint64_t* v, int n, RedOp op, std::string*) override {
     b_->red[(size_t)r_].assign(v, v + n);
     b_->barrier();
@@ -424,6 +440,9 @@ LocalBoard* local_board_new(tlcg_ctx* const* ctxs, int n) {
   b->ctxs.assign(ctxs, ctxs + n);
   b->rows.assign((size_t)n * row_width(n), 0);
   b->red.resize((size_t)n);
+  const char* pv = std::getenv("TLCG_PULL");
+  b->pull = !(pv && !std::strcmp(pv, "0"));
+  for (int r = 1; r < n; ++r) b->pull = b->pull && ctx_device(ctxs[r]) == ctx_device(ctxs[0]);
   for (int r = 0; r < n; ++r) b->ts.emplace_back(new LocalTransport(b, r));
   return b;
 }
@@ -491,7 +510,7 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
         row[(size_t)d] = send[(size_t)d] = k;
       }
       row[(size_t)n] = failed ? 1 : 0;
-      row[(size_t)n + 1] = ctx_inbox_cap(c);
+      row[(size_t)n + 1] = t.can_pull() ? ~0ull : ctx_inbox_cap(c);  // (no inbox when pulling)
       row[(size_t)n + 2] = level;
       row[(size_t)n + 3] = erred ? 1 : 0;
       if (!t.allgather_rows(row.data(), rows.data(), err)) return -20;
@@ -524,15 +543,26 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
         if (bad) break;
       }
       tick(3, tp);
-      std::string rerr;
-      const bool moved = t.records(c, send.data(), recv.data(), &rerr);
-      tick(4, tp);
-      if (!moved) {  // (local failure: the transport's collective itself completed)
-        failed = true;
-        local_err = rerr;
-        continue;
+      if (t.can_pull()) {
+        // the sources' outboxes read in place; every rank passes pulled()
+        // (a failed one too), so no outbox is overwritten while read
+        std::vector<const uint64_t*> src;
+        std::vector<uint64_t> cnt;
+        t.pull_sources(c, recv.data(), &src, &cnt);
+        tick(4, tp);
+        if (!failed && ctx_absorb_from(c, src.data(), cnt.data(), (int)src.size(), &s) != 0) fail_local("absorb");
+        t.pulled();
+      } else {
+        std::string rerr;
+        const bool moved = t.records(c, send.data(), recv.data(), &rerr);
+        tick(4, tp);
+        if (!moved) {  // (local failure: the transport's collective itself completed)
+          failed = true;
+          local_err = rerr;
+          continue;
+        }
+        if (tlcg_absorb(c, total, &s) != 0) fail_local("tlcg_absorb");
       }
-      if (tlcg_absorb(c, total, &s) != 0) fail_local("tlcg_absorb");
       tick(5, tp);
       if (!failed && tlcg_end_level(c, &s) != 0) fail_local("tlcg_end_level");
       tick(6, tp);

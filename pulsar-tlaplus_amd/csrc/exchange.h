@@ -45,6 +45,14 @@ class Transport {
   // context's stream.
   virtual bool records(tlcg_ctx* c, const uint64_t* send, const uint64_t* recv, std::string* err) = 0;
   virtual bool allreduce(uint64_t* v, int n, RedOp op, std::string* err) = 0;
+  // Ranks that share one device need no copy: the destination's absorb reads
+  // every source's outbox in place.  can_pull() says this transport does so;
+  // pull_sources() gives one {records, count} per source for ctx (recv[s] =
+  // the count from rank s); pulled() returns once every rank's absorb is done
+  // with the outboxes (no source expands over its outbox before).
+  virtual bool can_pull() const { return false; }
+  virtual void pull_sources(tlcg_ctx*, const uint64_t*, std::vector<const uint64_t*>*, std::vector<uint64_t>*) {}
+  virtual void pulled() {}
 };
 
 // The check of one rank; *st, levels and the return value are the combined
@@ -76,6 +84,10 @@ void ctx_set_error(tlcg_ctx* c, const std::string& e);
 // forget the last tlcg_expand (its level is never absorbed: the loop ends):
 // the generated counts and the pending states as before it; fresh stats
 void ctx_undo_expand(tlcg_ctx* c, tlcg_stats* st);
+// tlcg_absorb of the records of n sources read where they lie (device memory
+// of the context's device): records[i] holds counts[i] {state, parent_ref}
+// records.  The local transport's pull: the other ranks' outboxes, no copy.
+int ctx_absorb_from(tlcg_ctx* c, const uint64_t* const* records, const uint64_t* counts, int n, tlcg_stats* st);
 
 // The local transport of n ranks driven by n threads of this process.
 struct LocalBoard;

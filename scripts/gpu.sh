@@ -12,6 +12,7 @@
 #   pmc:NAME:KERNEL:CASE          PMC groups of one check (scripts/pmc_kernel.sh CASE KERNEL NAME)
 #   probe:NAME:CASE,CASE,...      scripts/probe.py CASEs -> gpurun_out/probe_NAME.jsonl
 #   node:NAME:ARGS                scripts/node_bench.py ARGS -> gpurun_out/node_NAME.jsonl
+#   nodeprof:NAME:ARGS            rocprofv3 --kernel-trace of node_bench ARGS -> gpurun_out/timeline_NAME.jsonl
 #   py:NAME:SCRIPT,ARGS           python SCRIPT ARGS -> gpurun_out/py_NAME.log
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -66,6 +67,15 @@ for step in "$@"; do
       timeout -k 10 600 python -u scripts/node_bench.py "${args[@]}" > "gpurun_out/node_$name.jsonl" 2>&1 \
         || { echo "node $name failed"; tail -20 "gpurun_out/node_$name.jsonl"; exit 1; }
       cut -c1-400 "gpurun_out/node_$name.jsonl" ;;
+    nodeprof)
+      name="${rest%%:*}"; a="${rest#*:}"; [ "$a" = "$rest" ] && a=""
+      IFS=',' read -r -a args <<< "$a"
+      timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/nodeprof_$name" -o run \
+        -- python3 -u scripts/node_bench.py "${args[@]}" > "gpurun_out/nodeprof_$name.log" 2>&1 \
+        || { echo "nodeprof $name failed"; tail -20 "gpurun_out/nodeprof_$name.log"; exit 1; }
+      f=$(ls gpurun_out/nodeprof_$name/*/run_kernel_trace.csv gpurun_out/nodeprof_$name/run_kernel_trace.csv 2>/dev/null | head -1)
+      [ -n "$f" ] && python3 scripts/timeline.py "$f" > "gpurun_out/timeline_$name.jsonl" && cut -c1-600 "gpurun_out/timeline_$name.jsonl"
+      ;;
     py)
       name="${rest%%:*}"; a="${rest#*:}"
       IFS=',' read -r -a args <<< "$a"
