@@ -567,7 +567,9 @@ def main():
             kern = ("tlcg_tree_384 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<384, 512, 4> (") + \
                 "component tree, 4 components per wavefront)"
         else:
-            kern = ("tlcg_treec_640 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<640, 1024, 4, closed> (") + \
+            kern = "tlcg_treecw_640 (hipRTC-specialized, component tree closed mode: component codes, one " \
+                "code-graph walk per wavefront, lane-interleaved store)" if r["jit"] & 16 else \
+                ("tlcg_treec_640 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<640, 1024, 4, closed> (") + \
                 "component tree closed mode: component codes, 4 components per wavefront)"
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kern,

@@ -169,7 +169,9 @@ typedef struct tlcg_stats {
                                 bit 2: user invariants: the global engine's check is device code
                                 (hipRTC, tlcg_user_check), not the interpreter;
                                 bit 3: the code pass walked each code graph once per wavefront
-                                for its components (tlcg_componentw_64, component_wave.h) */
+                                for its components (tlcg_componentw_64, component_wave.h);
+                                bit 4: the component tree's closed mode did the same
+                                (tlcg_treecw_640, tree_wave.h: its store is lane-interleaved) */
   uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
   uint64_t fpset_host_states; /* states held by the host FPSet tier (tlcg_opts.fpset_spill) */
   uint64_t transport;        /* multi-rank runs: 1 host threads + device copies, 2 RCCL; 0 one context */

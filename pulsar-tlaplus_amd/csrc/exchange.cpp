@@ -123,7 +123,7 @@ class RcclTransport : public Transport {
     return true;
   }
 
-  bool records(tlcg_ctx* c, const uint64_t* send, const uint64_t* recv, std::string* err) override {
+  bool records(tlcg_ctx* c, const uint64_t* send, const uint64_t* recv, std::string* err, bool wait_done) override {
     uint64_t total = 0;
     for (int r = 0; r < s_->world; ++r)
       if (r != s_->rank) total += recv[r];
@@ -156,9 +156,14 @@ class RcclTransport : public Transport {
     }
     // the absorb that follows is ordered on the stream; waiting here puts the
     // records under TLCG_COMM_TIMEOUT_S too (a peer that died mid-exchange
-    // aborts the communicator instead of hanging the absorb)
-    return nccl(R()->GroupEnd(), "ncclGroupEnd", err) && wait(err);
+    // aborts the communicator instead of hanging the absorb).
+    // Without the wait (the pipelined level) the level's one wait_stream()
+    // does the same.
+    return nccl(R()->GroupEnd(), "ncclGroupEnd", err) && (!wait_done || wait(err));
   }
+
+  bool can_pipeline() const override { return true; }
+  bool wait_stream(tlcg_ctx*, std::string* err) override { return wait(err); }
 
   bool allreduce(uint64_t* v, int n, RedOp op, std::string* err) override {
     if (n <= 0) return true;
@@ -369,7 +374,7 @@ class LocalTransport : public Transport {
 
   // the destination pulls: every source's outbox for this rank, device to
   // device (over xGMI between GPUs), source-rank-major into the inbox
-  bool records(tlcg_ctx* c, const uint64_t*, const uint64_t* recv, std::string* err) override {
+  bool records(tlcg_ctx* c, const uint64_t*, const uint64_t* recv, std::string* err, bool) override {
     uint64_t total = 0;
     for (int s = 0; s < b_->n; ++s)
       if (s != r_) total += recv[s];
@@ -400,19 +405,27 @@ class LocalTransport : public Transport {
   }
 
   bool can_pull() const override { return b_->pull; }
-  void pull_sources(tlcg_ctx*, const uint64_t* recv, std::vector<const uint64_t*>* p,
+  // every source's records for this rank where the source's row says its
+  // outbox lies (its address as of the all-gather: a pipelined source may
+  // already be expanding into its other outbox)
+  void pull_sources(tlcg_ctx*, const uint64_t* rows, std::vector<const uint64_t*>* p,
                     std::vector<uint64_t>* k) override {
+    const int n = b_->n;
+    const size_t w = row_width(n);
     p->clear();
     k->clear();
-    for (int s = 0; s < b_->n; ++s) {
-      if (s == r_ || !recv[s]) continue;
-      void* q = nullptr;
-      tlcg_outbox(b_->ctxs[(size_t)s], r_, &q, nullptr);
-      p->push_back(static_cast<const uint64_t*>(q));
-      k->push_back(recv[s]);
+    for (int s = 0; s < n; ++s) {
+      const uint64_t* row = rows + (size_t)s * w;
+      if (s == r_ || !row[r_]) continue;
+      const auto* base = reinterpret_cast<const uint64_t*>((uintptr_t)row[n + 4]);
+      p->push_back(base + 2 * (uint64_t)r_ * row[n + 5]);
+      k->push_back(row[r_]);
     }
   }
   void pulled() override { b_->barrier(); }
+  // pulling ranks need no barrier after the absorb when the outboxes are
+  // double-buffered (ctx_absorb_expand)
+  bool can_pipeline() const override { return b_->pull; }
 
   bool allreduce(uint64_t* v, int n, RedOp op, std::string*) override {
     b_->red[(size_t)r_].assign(v, v + n);
@@ -448,6 +461,13 @@ LocalBoard* local_board_new(tlcg_ctx* const* ctxs, int n) {
 }
 void local_board_free(LocalBoard* b) { delete b; }
 Transport* local_transport(LocalBoard* b, int rank) { return b->ts[(size_t)rank].get(); }
+
+bool Transport::wait_stream(tlcg_ctx* c, std::string* err) {
+  const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(tlcg_stream(c)));
+  if (e == hipSuccess) return true;
+  *err = std::string("stream: ") + hipGetErrorString(e);
+  return false;
+}
 
 // ------------------------------------------------------------ the loop -----
 
@@ -490,6 +510,10 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
       if (tlcg_init(c, &s) != 0) fail_local("tlcg_init");
     }
     std::vector<uint64_t> row(w), rows(w * (size_t)n), send((size_t)n), recv((size_t)n);
+    // one host synchronization per level (ctx_absorb_expand) when both the
+    // transport and the level's kernels allow it; every rank decides alike
+    const bool pipe = !all_tree && t.can_pipeline() && ctx_pipeline_ok(c);
+    bool have = false;  // pipe: this rank's next level is already expanded
     for (; !all_tree;) {
       auto tp = clk();
       // expand this rank's newest level (an empty one too: every rank takes
@@ -499,10 +523,13 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
       // empty, an error, a failure), the expand is undone -- its level is
       // never absorbed -- so the counts are those of the level loop that
       // decided first (round 3 ran a separate all-reduce before each expand).
+      // Pipelined, the expand after the first level's happened inside the
+      // previous iteration's ctx_absorb_expand.
       const uint64_t level = failed ? 0 : s.frontier;
       const bool erred = !failed && s.status >= TLCG_VIOLATION;
       const bool live = !failed && s.status == TLCG_RUNNING;
-      if (live && tlcg_expand(c, &s) != 0) fail_local("tlcg_expand");
+      if (live && !have && tlcg_expand(c, &s) != 0) fail_local("tlcg_expand");
+      have = false;
       tick(1, tp);
       for (int d = 0; d < n; ++d) {
         uint64_t k = 0;
@@ -513,6 +540,7 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
       row[(size_t)n + 1] = t.can_pull() ? ~0ull : ctx_inbox_cap(c);  // (no inbox when pulling)
       row[(size_t)n + 2] = level;
       row[(size_t)n + 3] = erred ? 1 : 0;
+      ctx_outbox(c, &row[(size_t)n + 4], &row[(size_t)n + 5]);
       if (!t.allgather_rows(row.data(), rows.data(), err)) return -20;
       tick(2, tp);
       bool any = false, grow = false, stop = false;
@@ -543,26 +571,38 @@ int run_ranks(tlcg_ctx* c, Transport& t, tlcg_stats* st, std::vector<uint64_t>* 
         if (bad) break;
       }
       tick(3, tp);
+      std::vector<const uint64_t*> src;
+      std::vector<uint64_t> cnt;
       if (t.can_pull()) {
-        // the sources' outboxes read in place; every rank passes pulled()
-        // (a failed one too), so no outbox is overwritten while read
-        std::vector<const uint64_t*> src;
-        std::vector<uint64_t> cnt;
-        t.pull_sources(c, recv.data(), &src, &cnt);
-        tick(4, tp);
-        if (!failed && ctx_absorb_from(c, src.data(), cnt.data(), (int)src.size(), &s) != 0) fail_local("absorb");
-        t.pulled();
+        // the sources' outboxes read in place, where their rows say they lie
+        t.pull_sources(c, rows.data(), &src, &cnt);
       } else {
         std::string rerr;
-        const bool moved = t.records(c, send.data(), recv.data(), &rerr);
-        tick(4, tp);
+        const bool moved = t.records(c, send.data(), recv.data(), &rerr, !pipe);
         if (!moved) {  // (local failure: the transport's collective itself completed)
           failed = true;
           local_err = rerr;
           continue;
         }
-        if (tlcg_absorb(c, total, &s) != 0) fail_local("tlcg_absorb");
+        void* in = nullptr;
+        tlcg_inbox(c, 0, &in);
+        src.push_back(static_cast<const uint64_t*>(in));
+        cnt.push_back(total);
       }
+      tick(4, tp);
+      if (pipe) {
+        // absorb, end of level and the next level's expand, one wait; the
+        // outboxes are double-buffered, so no rank waits for the others here
+        if (!failed && ctx_absorb_expand(c, src.data(), cnt.data(), (int)src.size(), t, &s) != 0)
+          fail_local("absorb + expand");
+        have = !failed && s.status == TLCG_RUNNING;
+        tick(5, tp);
+        continue;
+      }
+      if (!failed && ctx_absorb_from(c, src.data(), cnt.data(), (int)src.size(), &s) != 0) fail_local("absorb");
+      // every rank passes pulled() (a failed one too), so no outbox is
+      // overwritten while another rank reads it
+      if (t.can_pull()) t.pulled();
       tick(5, tp);
       if (!failed && tlcg_end_level(c, &s) != 0) fail_local("tlcg_end_level");
       tick(6, tp);

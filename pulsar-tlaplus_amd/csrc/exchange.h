@@ -27,8 +27,9 @@ enum RedOp { RED_SUM = 0, RED_MIN = 1, RED_MAX = 2 };
 
 // words of a rank's row in the per-level all-gather: its record count per
 // destination, its failure flag, its inbox capacity, the size of the level it
-// expanded, its error flag (run_ranks)
-inline size_t row_width(int world) { return (size_t)world + 4; }
+// expanded, its error flag, its outbox's device address and its records per
+// destination (run_ranks)
+inline size_t row_width(int world) { return (size_t)world + 6; }
 
 class Transport {
  public:
@@ -43,7 +44,8 @@ class Transport {
   // every outbox of ctx to its owner; the inbox (already sized for the sum of
   // recv) receives them source-rank-major.  Ordered before later work on the
   // context's stream.
-  virtual bool records(tlcg_ctx* c, const uint64_t* send, const uint64_t* recv, std::string* err) = 0;
+  virtual bool records(tlcg_ctx* c, const uint64_t* send, const uint64_t* recv, std::string* err,
+                       bool wait = true) = 0;
   virtual bool allreduce(uint64_t* v, int n, RedOp op, std::string* err) = 0;
   // Ranks that share one device need no copy: the destination's absorb reads
   // every source's outbox in place.  can_pull() says this transport does so;
@@ -51,8 +53,17 @@ class Transport {
   // the count from rank s); pulled() returns once every rank's absorb is done
   // with the outboxes (no source expands over its outbox before).
   virtual bool can_pull() const { return false; }
-  virtual void pull_sources(tlcg_ctx*, const uint64_t*, std::vector<const uint64_t*>*, std::vector<uint64_t>*) {}
+  // rows: the level's all-gathered rows (row_width(world) words each, whose
+  // words world + 4 / world + 5 hold each rank's outbox address and its
+  // records per destination)
+  virtual void pull_sources(tlcg_ctx*, const uint64_t* /*rows*/, std::vector<const uint64_t*>*,
+                            std::vector<uint64_t>*) {}
   virtual void pulled() {}
+  // The one-synchronization level (ctx_absorb_expand): the transport moves
+  // a level's records without waiting for them (records(..., wait = false))
+  // and wait_stream() is the level's one wait on the context's stream.
+  virtual bool can_pipeline() const { return false; }
+  virtual bool wait_stream(tlcg_ctx* c, std::string* err);
 };
 
 // The check of one rank; *st, levels and the return value are the combined
@@ -88,6 +99,14 @@ void ctx_undo_expand(tlcg_ctx* c, tlcg_stats* st);
 // of the context's device): records[i] holds counts[i] {state, parent_ref}
 // records.  The local transport's pull: the other ranks' outboxes, no copy.
 int ctx_absorb_from(tlcg_ctx* c, const uint64_t* const* records, const uint64_t* counts, int n, tlcg_stats* st);
+// the same absorb, then tlcg_end_level, then (the search going on) the next
+// level's tlcg_expand, with one wait on the stream (t.wait_stream) when
+// ctx_pipeline_ok(c); the records must be readable in stream order
+int ctx_absorb_expand(tlcg_ctx* c, const uint64_t* const* records, const uint64_t* counts, int n, Transport& t,
+                      tlcg_stats* st);
+bool ctx_pipeline_ok(const tlcg_ctx* c);
+// device address of c's current outbox and its records per destination
+void ctx_outbox(const tlcg_ctx* c, uint64_t* addr, uint64_t* per_dst);
 
 // The local transport of n ranks driven by n threads of this process.
 struct LocalBoard;

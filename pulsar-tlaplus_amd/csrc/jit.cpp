@@ -73,6 +73,9 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
     for (const char* od : {"false", "true"})
       s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_componentw") +
            (od[0] == 't' ? "od" : "") + "_64(tlcg::CompArgs a) { tlcg::component_wave_body<64, " + od + ">(a, kL); }\n";
+    // the component tree's closed mode, one walk per wave (tree_wave.h)
+    s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treecw_640(tlcg::TreeArgs a) "
+         "{ tlcg::tree_wave_body<640, " + w + ">(a, kL); }\n";
     return s;
   }
   for (int K : {32, 64, 128, 255})
@@ -252,8 +255,9 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
   out->compile_s += wcs;
   out->wave_m = user.empty() ? WAVE_M : WAVE_M_USER;  // (component_wave.h TLCG_WAVE_M)
   if (hipModuleGetFunction(&out->wave[0], out->wave_module, "tlcg_componentw_64") != hipSuccess ||
-      hipModuleGetFunction(&out->wave[1], out->wave_module, "tlcg_componentwod_64") != hipSuccess) {
-    *err = "hipModuleGetFunction tlcg_componentw_64";
+      hipModuleGetFunction(&out->wave[1], out->wave_module, "tlcg_componentwod_64") != hipSuccess ||
+      hipModuleGetFunction(&out->treew, out->wave_module, "tlcg_treecw_640") != hipSuccess) {
+    *err = "hipModuleGetFunction tlcg_componentw_64 / tlcg_treecw_640";
     return false;
   }
   const char* names[4] = {"32", "64", "128", "255"};
@@ -300,6 +304,16 @@ bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool co
   CompArgs copy = a;
   void* args[] = {&copy};
   return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
+}
+
+bool jit_launch_tree_wave(const JitKernels& k, const TreeArgs& a, hipStream_t stream) {
+  if (!a.n_comp) return true;
+  if (!k.treew) return false;
+  TreeArgs copy = a;
+  void* args[] = {&copy};
+  // one wave per TLCG_TREE_WAVE_M batches of 64 components (the kernel strides over the rest)
+  return hipModuleLaunchKernel(k.treew, tree_grid((a.n_comp + 63) / 64, TREE_WAVE_M), 1, 1, 64, 1, 1, 0, stream, args,
+                               nullptr) == hipSuccess;
 }
 
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream) {

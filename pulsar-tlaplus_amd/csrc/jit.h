@@ -24,6 +24,7 @@ struct JitKernels {
   hipFunction_t code[2] = {nullptr, nullptr};     // component codes (component_code.h), K = 32, 64
   hipFunction_t code_od[2] = {nullptr, nullptr};
   hipFunction_t wave[2] = {nullptr, nullptr};     // codes, K = 64, one walk per wave (component_wave.h); outdegrees
+  hipFunction_t treew = nullptr;                  // the tree's closed mode at 640 states, one walk per wave (tree_wave.h)
   int wave_m = WAVE_M;                            // its components per lane (the grid)
   hipFunction_t tree[4] = {nullptr, nullptr, nullptr, nullptr};  // component tree: 384 x 4 groups, 1024 x 1;
                                                                  // closed mode: 640 x 4, 2048 x 1
@@ -58,6 +59,9 @@ bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStr
 
 // the specialized tree kernel for cap 384 / 640 (4 groups) or 1024 / 2048 (1 group); false when not built or on a
 // launch error
+// the closed tree at 640 states with one walk per wave (tree_wave.h: the
+// lane-interleaved store, tree_wave_slot)
+bool jit_launch_tree_wave(const JitKernels& k, const TreeArgs& a, hipStream_t stream);
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream);
 
 }  // namespace tlcg

@@ -406,6 +406,7 @@ class Result:
     trace: List[Tuple[str, int]] = field(default_factory=list)
     transport: str = ""  # multi-rank runs: "local" (threads, device copies) or "rccl"
     tlc_exact: bool = False  # an error whose trace and tlc_stop_stats() are TLC -workers 1's (tlcg_stats.tlc_exact)
+    jit_used: int = 0  # tlcg_stats.jit_used: which specialized kernels ran (include/tlcgpu.h)
 
 
 class Checker:
@@ -528,7 +529,7 @@ class Checker:
                    collision_optimistic=s.fp_collision_optimistic, kernel_ms=s.kernel_ms,
                    expand_ms=s.expand_ms, levels_redone=s.levels_redone,
                    engine={v: k for k, v in ENGINES.items()}.get(s.engine, "?"), host_states=s.host_states,
-                   fpset_host_states=s.fpset_host_states, tlc_exact=bool(s.tlc_exact))
+                   fpset_host_states=s.fpset_host_states, tlc_exact=bool(s.tlc_exact), jit_used=s.jit_used)
         if s.invariant >= 0:
             r.invariant = self.model.invariants[s.invariant]
         if s.action >= 0:

@@ -107,6 +107,29 @@ def test_run_node_violation_verdict(case, partition, ranks):
     assert (r.status, r.invariant, r.depth) == (want["result"], want["invariant"], want["depth"])
 
 
+@pytest.mark.parametrize("pipeline", ["1", "0"])
+@pytest.mark.parametrize("case", ["S", "V_leak"])
+def test_run_node_pipelined_level_overflows(case, pipeline, monkeypatch):
+    """the one-wait level (csrc/tlcgpu.hip ctx_absorb_expand: absorb, end of
+    level and next expand on the stream back to back) and the two-step level
+    (TLCG_PIPELINE=0) report the same counts and verdict when the outboxes
+    start at 64 records per destination (TLCG_OUTBOX_CAP) and overflow, so
+    the expand's redo paths run, from tiny store and FPSet sizes"""
+    monkeypatch.setenv("TLCG_PIPELINE", pipeline)
+    monkeypatch.setenv("TLCG_OUTBOX_CAP", "64")  # the first outbox of each buffer overflows
+    want = GOLDEN[case]["result"]
+    r = tlcgpu.run_node(model_of(GOLDEN[case]["constants"]), 3, partition=2, engine="global", log2_fpset_slots=8,
+                        state_capacity=256)
+    assert r.status == want["result"]
+    if want["result"] == "ok":
+        assert (r.generated, r.distinct, r.depth, r.levels) == (want["generated"], want["distinct"], want["depth"],
+                                                                 want["levels"])
+    else:
+        assert (r.invariant, r.depth) == (want["invariant"], want["depth"])
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+    assert r.levels_redone > 0
+
+
 def test_run_node_matches_checker_engines():
     # the closed partition runs either engine per rank; the open one the global engine
     m = model_of(GOLDEN["S"]["constants"])

@@ -236,17 +236,25 @@ def test_tree_sharded_error_hands_over_to_the_exchange(case):
     assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
 
 
-def test_tree_closed_store_reads_back_states():
+@pytest.mark.parametrize("jit", ["0", "1"])
+def test_tree_closed_store_reads_back_states(jit, monkeypatch):
     """the closed mode stores component codes (tree_body.h TLCG_TREE_CODE_STORE);
     tlcg_copy_states / tlcg_state_at decode them: the first component's chunk
     holds exactly its reachable states, each one's parent reference names a
-    state of the chunk that has it as a successor"""
+    state of the chunk that has it as a successor.  TLCG_JIT=1: the hipRTC
+    kernels, whose first pass walks each code graph once per wavefront
+    (tree_wave.h) into a lane-interleaved store: component 0's position i is
+    slot 64 i (tree_wave_slot)"""
+    monkeypatch.setenv("TLCG_JIT", jit)
     c = GOLDEN["W_C12_k1"]["constants"]
     m = model_of(c)
     ck = tlcgpu.Checker(m)
     try:
         r = ck.run()
         assert r.engine == "tree"
+        wave = bool(r.jit_used & 16)
+        assert wave == (jit == "1")
+        step = 64 if wave else 1  # slot of component 0's next position
         s0 = tlcgpu.host_init_state(m, 0)
         seen, todo = set(), [s0]
         while todo:
@@ -256,13 +264,15 @@ def test_tree_closed_store_reads_back_states():
                 todo += [t for _, t in tlcgpu.host_successors(m, s)]
         n = len(seen)
         assert n == r.distinct // tlcgpu.init_count(m)
-        stored = ck.copy_states(0, n)
+        stored = ck.copy_states(0, n * step)[::step]
         assert set(stored) == seen and stored[0] == s0
         ob = tlcgpu.load_library().tlcg_ordinal_bits(C.byref(m.to_c()))
-        for g in range(1, n, 7):
-            s, p = ck.state_at(g)
-            assert s == stored[g]
-            ps, _ = ck.state_at((p & ((1 << 56) - 1)) >> ob)
+        for i in range(1, n, 7):
+            s, p = ck.state_at(i * step)
+            assert s == stored[i]
+            pg = (p & ((1 << 56) - 1)) >> ob
+            assert pg % step == 0
+            ps, _ = ck.state_at(pg)
             assert s in [t for _, t in tlcgpu.host_successors(m, ps)]
     finally:
         ck.close()
