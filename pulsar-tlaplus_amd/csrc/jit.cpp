@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 #include <vector>
@@ -254,6 +255,8 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
   if (!load_module(L, device, user, JIT_WAVE, &out->wave_module, &wcached, &wcs, err)) return false;
   out->compile_s += wcs;
   out->wave_m = user.empty() ? WAVE_M : WAVE_M_USER;  // (component_wave.h TLCG_WAVE_M)
+  if (const char* d = std::getenv("TLCG_JIT_DEFINES"))  // (a tuning build's own M: the record tables follow it)
+    if (const char* m = std::strstr(d, "TLCG_WAVE_M=")) out->wave_m = std::max(1, std::atoi(m + 12));
   if (hipModuleGetFunction(&out->wave[0], out->wave_module, "tlcg_componentw_64") != hipSuccess ||
       hipModuleGetFunction(&out->wave[1], out->wave_module, "tlcg_componentwod_64") != hipSuccess ||
       hipModuleGetFunction(&out->treew, out->wave_module, "tlcg_treecw_640") != hipSuccess) {

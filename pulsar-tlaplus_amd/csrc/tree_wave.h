@@ -15,9 +15,13 @@
 //   - the FIFO of codes and the FPSet (1 + queue position per slot) are the
 //     wave's, in LDS, read at wave-uniform addresses; the walk's control is
 //     scalar and its arithmetic vector (vcopy, component_wave.h);
-//   - each component still gets every state's code and parent reference in
-//     its own store slots, every state checked against every invariant of
-//     the cfg on its own constants (its `messages`: CodeConsts), its own
+//   - the walk's records (code, parent queue position, action) are the same
+//     for every component of the walk: they are stored once per walk and
+//     position (TreeArgs::walk_rec) and each component names its walk
+//     (walk_of); a component's slot (tree_wave_slot) keeps its numbering and
+//     decodes through its walk's record (tlcgpu.hip tree_wave_record);
+//   - each component still gets every state checked against every invariant
+//     of the cfg on its own constants (its `messages`: CodeConsts), its own
 //     least error key (tree_event_key) and its size; the per-depth counts are
 //     one add per depth for all the components of the walk.
 // Components that do not share the leader's code graph (another initial code
@@ -25,10 +29,10 @@
 // (its initial state does not round-trip) or past CAP states or TREE_MAXLV
 // depths raises TREE_OVERFLOW, as in tree_body.h (the 2048-state pass).
 //
-// Store layout: lane-interleaved, so the 64 lanes' stores of one queue
-// position are one contiguous run -- slot (ci, pos) = ((ci / 64) * CAP + pos)
-// * 64 + ci % 64 (tree_wave_slot; tlcgpu.hip tree_code_word decodes it); the
-// chunk layout of tree_body.h ([ci][CAP]) would spread them over 64 lines.
+// Slot numbering: lane-interleaved -- slot (ci, pos) = ((ci / 64) * CAP +
+// pos) * 64 + ci % 64 (tree_wave_slot), the layout in which the first
+// version stored every component's code and parent reference (12 B per
+// state: 2.62 ms for G9-deep, 0.57 of HBM peak, profiles/r05_bench_g9deep.json).
 #pragma once
 #if !defined(__HIPCC_RTC__)
 #include "component_wave.h"
@@ -75,12 +79,6 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       todo[m] = act && code_word<W>(L, ccon[m], s0 & messages_mask<W>(L), c0[m]) == s0;
       if (act && !todo[m]) flags |= TREE_OVERFLOW;  // no code
     }
-    // the batches' rows of the store (range-checked raw buffer stores; a
-    // component out of the walk stores past the range: the hardware drops it)
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<uint32_t*>(a.states) + b0 * (u64)CAP * 64, (short)0, M * CAP * 64 * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-        a.parents + b0 * (u64)CAP * 64, (short)0, M * CAP * 64 * 8, 0x00020000);
     for (;;) {
       // the walk's leader: the first component still to walk
       int lm = -1;
@@ -112,6 +110,20 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
         nin += in[m] ? 1 : 0;
       }
       const unsigned nwalk = uni((uint32_t)wave_sum_u64((u64)nin));  // components of this walk
+      // the walk's number: its records' row (past walk_cap: the 2048-state pass takes the model)
+      unsigned long long wid = 0;
+      if (lane == 0) wid = atomicAdd(a.walk_n, 1ull);
+      wid = __builtin_amdgcn_readfirstlane((unsigned)wid);
+      if (wid >= a.walk_cap) {
+        flags |= TREE_OVERFLOW;
+        break;
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (in[m]) a.walk_of[(b0 + m) * 64 + (u64)lane] = (uint32_t)wid;
+      // its records (range-checked raw buffer stores from lane 0)
+      const __amdgpu_buffer_rsrc_t rr =
+          __builtin_amdgcn_make_buffer_rsrc(a.walk_rec + wid * (u64)CAP, (short)0, CAP * 8, 0x00020000);
       CodeConsts cu{};  // the transitions read Len only
       cu.len = lenu;
       for (int i = lane; i < T; i += 64) h[i] = 0;
@@ -120,13 +132,11 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
         h[(cu0 * 0x9E3779B1u) >> (32 - TB)] = 1;
         q[0] = cu0;
       }
-      // position 0: the initial state
+      // position 0: the initial state (no parent)
+      __builtin_amdgcn_raw_buffer_store_b32(cu0, rr, lane == 0 ? 0 : 0x7fffffff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(0u, rr, lane == 0 ? 4 : 0x7fffffff, 0, 0);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const unsigned o = ((unsigned)m * CAP * 64u + (unsigned)lane);
-        __builtin_amdgcn_raw_buffer_store_b32(cu0, rc, in[m] ? (int)(o * 4) : 0x7fffffff, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)NO_PARENT, rp, in[m] ? (int)(o * 8) : 0x7fffffff, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(NO_PARENT >> 32), rp, in[m] ? (int)(o * 8 + 4) : 0x7fffffff, 0, 0);
         const int c = check_invariants_cb<W>(L, ccon[m], cu0);
         const u64 k = tree_event_key(0, a.comp0 + (b0 + m) * 64 + (u64)lane);
         evk = in[m] && c >= 0 ? min(evk, k) : evk;
@@ -163,14 +173,12 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
           }
           h[sl] = (uint16_t)(tail + 1);
           q[tail] = key;
+          // the walk's record of position tail: code, parent position, parent ordinal
+          __builtin_amdgcn_raw_buffer_store_b32(key, rr, lane == 0 ? tail * 8 : 0x7fffffff, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)head | (uint32_t)ord << 16, rr, lane == 0 ? tail * 8 + 4 : 0x7fffffff,
+                                                0, 0);
 #pragma unroll
           for (int m = 0; m < M; ++m) {
-            const unsigned o = ((unsigned)m * CAP + (unsigned)tail) * 64u + (unsigned)lane;
-            const u64 pslot = (((b0 + m) * CAP + (u64)head) << 6) + (u64)lane;
-            const u64 pref = a.rank_tag | ((a.gbase + pslot) << L.ord_bits) | (u64)ord;
-            __builtin_amdgcn_raw_buffer_store_b32(key, rc, in[m] ? (int)(o * 4) : 0x7fffffff, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)pref, rp, in[m] ? (int)(o * 8) : 0x7fffffff, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(pref >> 32), rp, in[m] ? (int)(o * 8 + 4) : 0x7fffffff, 0, 0);
             const int c = check_invariants_cb<W>(L, ccon[m], key);
             const u64 k = tree_event_key(level + 1, a.comp0 + (b0 + m) * 64 + (u64)lane);
             evk = in[m] && c >= 0 ? min(evk, k) : evk;

@@ -294,6 +294,39 @@ def test_g9_component_engine():
         ck.close()
 
 
+def test_g9_component_wave_records_decode():
+    """G9 on the component engine's wave kernel (csrc/component_wave.h): the
+    records are the walks' (one per walk and queue position), and every
+    component's slot still decodes (tlcgpu.hip crec_index, comp_slot_decode):
+    sampled components read back their initial state at position 0, and every
+    sampled state is a successor of its recorded parent (same lane, an earlier
+    position) by the recorded action"""
+    import ctypes
+    m = tlcgpu.Model(**G9)
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run(with_trace=False)
+        assert r.engine == "component" and r.jit_used & 8
+        assert r.distinct == 1_040_187_392
+        lib = tlcgpu.load_library()
+        ob = lib.tlcg_ordinal_bits(ctypes.byref(m.to_c()))
+        rng = random.Random(11)
+        for _ in range(200):
+            ci = rng.randrange(16 ** 6)
+            row = (ci // 64) * 64 * 64 + ci % 64  # (K = 64: slot = batch x 4096 + position x 64 + lane)
+            s0, p0 = ck.state_at(row)
+            assert s0 == tlcgpu.host_init_state(m, ci) and p0 == (1 << 64) - 1  # (NO_PARENT)
+            g = row + 64 * rng.randrange(1, 62)  # every G9 component holds 62 states
+            s, pref = ck.state_at(g)
+            pg, ordinal = (pref & ((1 << 56) - 1)) >> ob, pref & ((1 << ob) - 1)
+            assert pg % 64 == ci % 64 and row <= pg < g
+            ps, _ = ck.state_at(pg)
+            act = tlcgpu.ACTIONS[lib.tlcg_action_of_ordinal(ctypes.byref(m.to_c()), ordinal)]
+            assert (act, s) in tlcgpu.host_successors(m, ps)
+    finally:
+        ck.close()
+
+
 @pytest.mark.parametrize("case", ["X_keys3_vals57", "S_consumer", "S_noretain", "R_C3_K1"])
 @pytest.mark.parametrize("jit", ["0", "1"])
 def test_component_code_records_decode(jit, case, monkeypatch):
