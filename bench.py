@@ -76,7 +76,19 @@ BYTES_PER_STATE_WORD = 8
 
 # the newest round's profile of each kind (profiles/rNN_*), measured on the same kernels
 PMC_PROFILE = "pmc_k_expand.json"
-COMPONENT_BYTES_PER_STATE = 4  # the code pass writes one 32-bit record per state (component.h comp_record)
+COMPONENT_BYTES_PER_STATE = 4  # the per-lane code pass writes one 32-bit record per state (component.h comp_record)
+# the wave kernels (component_wave.h, tree_wave.h) write one record per walk and
+# queue position, a walk holding M x 64 components (component.h WAVE_M /
+# WAVE_M_USER, tree.h TREE_WAVE_M), plus, on the tree, each component's walk
+# number and size (2 x 4 B)
+WAVE_M, WAVE_M_USER, TREE_WAVE_M = 10, 2, 8
+
+
+def wave_kernel_bytes(comps, m, records, rec_bytes, per_comp=0):
+    """HBM bytes one wave-kernel launch writes: ceil(ceil(comps / 64) / m)
+    walks x `records` queue positions x rec_bytes, plus per_comp per component"""
+    walks = -(-(-(-comps // 64)) // m)
+    return walks * records * rec_bytes + comps * per_comp
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
 # SURVEY 8(d): algorithmic HBM bytes per distinct state of the BFS path (read
 # the frontier state 8 B, write the new state 8 B and its parent entry 8 B,
@@ -529,19 +541,27 @@ def main():
                     note="notional: the on-chip engines keep their FPSet and FIFO in LDS and never move these bytes")
 
     def roofline_component(r):
-        # the kernel's own algorithmic HBM bytes: one 4-B record written per
-        # distinct state (comp_record; its FIFO and FPSet stay in LDS, the
-        # components' constants come from the initial-state index; the 32-bit
-        # cascade passes, none on G9, write 16 B); SURVEY 8(d)'s 34.7 B/state
-        # (the HBM-FPSet design's) beside it as survey_equivalent
+        # the kernel's own algorithmic HBM bytes: the per-lane kernel writes
+        # one 4-B record per distinct state (comp_record; its FIFO and FPSet
+        # stay in LDS, the components' constants come from the initial-state
+        # index; the 32-bit cascade passes, none on G9, write 16 B); the wave
+        # kernel one record per walk and queue position (K = 64); SURVEY
+        # 8(d)'s 34.7 B/state (the HBM-FPSet design's) beside it as survey_equivalent
         kt = r["expand_ms"] * 1e-3
-        achieved = COMPONENT_BYTES_PER_STATE * distinct / world / kt / 1e9
+        comps = tlcgpu.init_count(model) // world
+        wave = bool(r["jit"] & 8)
+        kbytes = wave_kernel_bytes(comps, WAVE_M_USER if cfg.get("user") else WAVE_M, 64, 4) if wave else \
+            COMPONENT_BYTES_PER_STATE * distinct / world
+        achieved = kbytes / kt / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
                   kernel=component_kernel_name(r["jit"]),
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=COMPONENT_BYTES_PER_STATE,
-                  bytes_basis="the kernel's HBM bytes per distinct state: its 4-B store record (DESIGN 4)",
+                  bytes_per_distinct=round(kbytes * world / distinct, 4),
+                  bytes_basis="the kernel's HBM bytes per distinct state: " +
+                              ("one 4-B record per walk and queue position, a walk serving M x 64 components; the "
+                               "binding resource is the walk's issue (roofline.issue), not HBM (DESIGN 4)" if wave else
+                               "its 4-B store record (DESIGN 4)"),
                   survey_equivalent=survey_equivalent(r))
         # (each kernel priced with its own profile: component_<cfg> = the one walk per
         # wavefront, component_perlane_<cfg> = component_body.h's lanes)
@@ -552,7 +572,7 @@ def main():
                 new = new or pmc_fields(prof, rf["kernel"], kt, distinct)
         if new:
             rf.update(new)
-            rf["traffic_over_algorithmic"] = round(new["traffic_bytes_per_step"] / (COMPONENT_BYTES_PER_STATE * distinct), 3)
+            rf["traffic_over_algorithmic"] = round(new["traffic_bytes_per_step"] / kbytes, 3)
         return rf
 
     def roofline_tree(r):
@@ -562,6 +582,8 @@ def main():
         # state, 9 B per entry) or, closed, the 4-B component code the host
         # decodes (tree_body.h TLCG_TREE_CODE_STORE); its FPSets stay in LDS
         per_state = BYTES_PER_STATE_WORD * (words + 1) + 1 if open_model else 4 + BYTES_PER_STATE_WORD
+        if r["jit"] & 16:  # the closed wave kernel: 8-B records per walk and position, 8 B per component
+            per_state = wave_kernel_bytes(tlcgpu.init_count(model) // world, TREE_WAVE_M, 640, 8, 8) * world / distinct
         achieved = per_state * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
         if open_model:
             kern = ("tlcg_tree_384 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<384, 512, 4> (") + \
@@ -574,9 +596,12 @@ def main():
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                   frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kern,
                   launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=per_state,
-                  bytes_basis="the kernel's HBM bytes per distinct state: the stored state or code and its parent "
-                              "reference (DESIGN 4)",
+                  bytes_per_distinct=round(per_state, 4),
+                  bytes_basis="the kernel's HBM bytes per distinct state: " +
+                              ("its walks' 8-B records (one per walk and queue position, a walk serving M x 64 "
+                               "components) and each component's walk and size; the binding resource is the walk's "
+                               "issue (roofline.issue), not HBM (DESIGN 4)" if r["jit"] & 16 else
+                               "the stored state or code and its parent reference (DESIGN 4)"),
                   survey_equivalent=survey_equivalent(r))
         new = pmc_fields(f"tree_{args.config}", kern, r["expand_ms"] * 1e-3, distinct) if world == 1 else None
         if new:

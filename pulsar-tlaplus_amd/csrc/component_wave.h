@@ -129,14 +129,18 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
     // the components of the walk; the others (another code graph, or no code) go on to the cascade
     // (an event key goes to `ev` when found: a component that later leaves for
     // the cascade finds the same key again there)
-    bool run[M], stop[M];
+    // (per component: bit m of a vector register -- as bool arrays they are
+    // lane masks in scalar registers, 2 per component and flag, which at M = 10
+    // spill; profiles/r05_probe_wave_bits.jsonl)
+    uint32_t runb = 0, stopb = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const bool act = (b0 + m) * 64 + (u64)lane < a.n_comp;
-      run[m] = code_ok[m] && c0[m] == cu0 && ccon[m].len == lenu;
-      stop[m] = false;
-      if (act && !run[m]) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0(m);
+      const bool r = code_ok[m] && c0[m] == cu0 && ccon[m].len == lenu;
+      runb |= (uint32_t)r << m;
+      if (act && !r) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0(m);
     }
+    auto run = [&](int m) -> bool { return (runb >> m) & 1u; };
     CodeConsts cu{};  // the transitions read Len only
     cu.len = lenu;
     // component m's constants for its invariants (a component of the walk has the walk's Len)
@@ -169,11 +173,11 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
     __builtin_amdgcn_raw_buffer_store_b32(comp_record(cu0, 0, 0), rsrc, lane == 0 ? 0 : 0x7fffffff, 0, 0);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      if (run[m]) {
+      if (run(m)) {
         const int c = check_invariants_direct(L, kc(m), cu0);
         if (c >= 0) {  // an initial state violates: level 0 is complete, nothing is expanded
           ev = min(ev, (unsigned long long)make_comp_event(0, idx0(m), 0, 0, (c & 1) ? EVK_INV_ERROR : EVK_VIOLATION, c >> 1));
-          run[m] = false;
+          runb &= ~(1u << m);
           gen += 1;
           dist += 1;
           ++n0;
@@ -186,18 +190,8 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       if (lane == 0 && n) lvl_sh[0] += (unsigned long long)n;
     }
     __syncthreads();
-    auto any_run = [&]() -> bool {
-      bool r = false;
-#pragma unroll
-      for (int m = 0; m < M; ++m) r = r || run[m];
-      return __ballot(r) != 0;
-    };
-    auto n_run = [&]() -> int {
-      int n = 0;
-#pragma unroll
-      for (int m = 0; m < M; ++m) n += run[m] ? 1 : 0;
-      return (int)uni((uint32_t)wave_sum_u64((u64)n));
-    };
+    auto any_run = [&]() -> bool { return __ballot(runb != 0) != 0; };
+    auto n_run = [&]() -> int { return (int)uni((uint32_t)wave_sum_u64((u64)__popc(runb))); };
     int head = 0, tail = 1, level = 0, lvl_start = 0, lvl_end = 1;  // the walk's (scalar)
     unsigned lvgen = 0;
     uint32_t cur = vcopy(cu0);  // the walk's data: vector registers, the same in every lane
@@ -236,7 +230,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const int e = check_invariants_cbt(L, kc(m), key) + 1;
-          evk[m] = run[m] ? e : 0;
+          evk[m] = run(m) ? e : 0;
         }
         ++tail;
         __syncthreads();  // (the shared queue and table written)
@@ -258,11 +252,11 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       const bool walk_ev = (r == 2) | (nsucc == 0 && L.check_deadlock);
       bool any_ev = false;
 #pragma unroll
-      for (int m = 0; m < M; ++m) any_ev = any_ev | (run[m] & (walk_ev | (ev1[m] != 0) | (ev2[m] != 0)));
+      for (int m = 0; m < M; ++m) any_ev = any_ev | (run(m) & (walk_ev | (ev1[m] != 0) | (ev2[m] != 0)));
       if (any_ev) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        if (run[m] && (walk_ev | (ev1[m] != 0) | (ev2[m] != 0))) {
+        if (run(m) && (walk_ev | (ev1[m] != 0) | (ev2[m] != 0))) {
 #pragma nounroll
           for (int i = 0; i < 2; ++i) {  // an outcome table left it to the programs
             if ((i ? ev2[m] : ev1[m]) == INV_UNKNOWN + 1) {
@@ -281,7 +275,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
             k = min(k, make_comp_event(level + 1, idx0(m), head, ACT_CRASH,
                                        ((ev2[m] - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION, (ev2[m] - 1) >> 1));
           ev = min(ev, (unsigned long long)k);
-          stop[m] = stop[m] || k != NO_EVENT;
+          stopb |= (uint32_t)(k != NO_EVENT) << m;
         }
       }
       }
@@ -309,8 +303,8 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       if (ended || done || tail > K - 2)  // (the walk's conditions: most expansions skip this)
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const bool quit = run[m] && !deep && ((ended && stop[m]) || done);
-        const bool ovf = run[m] && !quit && (deep || tail > K - 2);
+        const bool quit = run(m) && !deep && ((ended && ((stopb >> m) & 1u)) || done);
+        const bool ovf = run(m) && !quit && (deep || tail > K - 2);
         if (ovf) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0(m) | ((u64)level << 40);  // levels < `level` counted
         if (quit) {
           // the last level [lvl_start, tail) was discovered, not expanded
@@ -323,7 +317,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
           }
           ++nq;
         }
-        run[m] = run[m] && !ovf && !quit;
+        if (ovf || quit) runb &= ~(1u << m);
       }
       const int nqw = (int)uni((uint32_t)wave_sum_u64((u64)nq));
       if (lane == 0 && nqw && tail > lvl_start) lvl_sh[level] += (unsigned long long)((tail - lvl_start) * nqw);

@@ -65,7 +65,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
   for (u64 b0 = (u64)blockIdx.x * M; b0 < nb; b0 += (u64)gridDim.x * M) {
     CodeConsts ccon[M];
     ckey c0[M];
-    bool todo[M];
+    uint32_t todob = 0;  // (per component: bit m of a vector register, not a lane mask in scalar registers)
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const u64 ci = (b0 + m) * 64 + (u64)lane;
@@ -76,8 +76,9 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       code_consts_user<W>(L, ccon[m]);  // the user invariants' outcome tables of this component
 #endif
       c0[m] = code_encode_w<W>(L, s0);
-      todo[m] = act && code_word<W>(L, ccon[m], s0 & messages_mask<W>(L), c0[m]) == s0;
-      if (act && !todo[m]) flags |= TREE_OVERFLOW;  // no code
+      const bool ok = act && code_word<W>(L, ccon[m], s0 & messages_mask<W>(L), c0[m]) == s0;
+      todob |= (uint32_t)ok << m;
+      if (act && !ok) flags |= TREE_OVERFLOW;  // no code
     }
     for (;;) {
       // the walk's leader: the first component still to walk
@@ -86,7 +87,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
 #pragma unroll
       for (int m = 0; m < M; ++m)
         if (lm < 0) {
-          lmask = __ballot(todo[m]);
+          lmask = __ballot((todob >> m) & 1u);
           if (lmask) lm = m;
         }
       if (lm < 0) break;
@@ -101,14 +102,12 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
         }
       const ckey cu0 = (ckey)__builtin_amdgcn_readlane((int)lc, leader);
       const uint32_t lenu = (uint32_t)__builtin_amdgcn_readlane((int)ll, leader);
-      bool in[M];
-      int nin = 0;
+      uint32_t inb = 0;
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        in[m] = todo[m] && c0[m] == cu0 && ccon[m].len == lenu;
-        todo[m] = todo[m] && !in[m];
-        nin += in[m] ? 1 : 0;
-      }
+      for (int m = 0; m < M; ++m) inb |= (uint32_t)(((todob >> m) & 1u) && c0[m] == cu0 && ccon[m].len == lenu) << m;
+      todob &= ~inb;
+      const int nin = __popc(inb);
+      auto in = [&](int m) -> bool { return (inb >> m) & 1u; };
       const unsigned nwalk = uni((uint32_t)wave_sum_u64((u64)nin));  // components of this walk
       // the walk's number: its records' row (past walk_cap: the 2048-state pass takes the model)
       unsigned long long wid = 0;
@@ -120,7 +119,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       }
 #pragma unroll
       for (int m = 0; m < M; ++m)
-        if (in[m]) a.walk_of[(b0 + m) * 64 + (u64)lane] = (uint32_t)wid;
+        if (in(m)) a.walk_of[(b0 + m) * 64 + (u64)lane] = (uint32_t)wid;
       // its records (range-checked raw buffer stores from lane 0)
       const __amdgpu_buffer_rsrc_t rr =
           __builtin_amdgcn_make_buffer_rsrc(a.walk_rec + wid * (u64)CAP, (short)0, CAP * 8, 0x00020000);
@@ -139,7 +138,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       for (int m = 0; m < M; ++m) {
         const int c = check_invariants_cb<W>(L, ccon[m], cu0);
         const u64 k = tree_event_key(0, a.comp0 + (b0 + m) * 64 + (u64)lane);
-        evk = in[m] && c >= 0 ? min(evk, k) : evk;
+        evk = in(m) && c >= 0 ? min(evk, k) : evk;
       }
       __syncthreads();
       int head = 0, tail = 1, level = 0, lvl_start = 0, lvl_end = 1;  // the walk's (scalar)
@@ -181,7 +180,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
           for (int m = 0; m < M; ++m) {
             const int c = check_invariants_cb<W>(L, ccon[m], key);
             const u64 k = tree_event_key(level + 1, a.comp0 + (b0 + m) * 64 + (u64)lane);
-            evk = in[m] && c >= 0 ? min(evk, k) : evk;
+            evk = in(m) && c >= 0 ? min(evk, k) : evk;
           }
           ++tail;
           __syncthreads();  // (the shared queue and table written)
@@ -201,7 +200,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
 #pragma unroll
           for (int m = 0; m < M; ++m) {
             const u64 k = tree_event_key(level + 1, a.comp0 + (b0 + m) * 64 + (u64)lane);
-            evk = in[m] ? min(evk, k) : evk;
+            evk = in(m) ? min(evk, k) : evk;
           }
         }
         ++head;
@@ -222,7 +221,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const u64 ci = (b0 + m) * 64 + (u64)lane;
-        if (in[m]) a.n_out[ci] = (uint32_t)tail;
+        if (in(m)) a.n_out[ci] = (uint32_t)tail;
       }
       if (full && nwalk) flags |= TREE_OVERFLOW;
       maxn = nwalk && (uint32_t)tail > maxn ? (uint32_t)tail : maxn;
