@@ -206,13 +206,14 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       action = (int)uni((uint32_t)action);
       int nsucc = 0;
       uint32_t first_new = 0;
-      int ev1[M], ev2[M];  // each component's first failing invariant + 1 of an inserted successor
-#pragma unroll
-      for (int m = 0; m < M; ++m) ev1[m] = ev2[m] = 0;
+      // bit m: component m's inserted successor (the compactor's, BrokerCrash's)
+      // may violate (its outcome is worked out again in the rare branch: one
+      // register each instead of one per component)
+      uint32_t evb1 = 0, evb2 = 0;
       // FPSet.put of one successor: a probe of the shared table, and on a miss
       // the insert (the queue; each component's record and invariants).
       // Returns whether it inserted (wave-uniform: the walk's control stays scalar)
-      auto put = [&](uint32_t key, int act_id, int* evk) -> bool {
+      auto put = [&](uint32_t key, int act_id, uint32_t* evb) -> bool {
         unsigned sl = slot_of<T>(key, a.mult);
         unsigned e = h[sl];
         for (int p = 0; uni(e) != 0 && p < T; ++p) {
@@ -227,22 +228,21 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
         // component's invariants, with no branch per component: a component
         // out of the walk has its outcome masked
         __builtin_amdgcn_raw_buffer_store_b32(comp_record(key, head, act_id), rsrc, lane == 0 ? tail * 4 : 0x7fffffff, 0, 0);
+        uint32_t b = 0;
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const int e = check_invariants_cbt(L, kc(m), key) + 1;
-          evk[m] = run(m) ? e : 0;
-        }
+        for (int m = 0; m < M; ++m) b |= (uint32_t)(check_invariants_cbt(L, kc(m), key) != -1) << m;
+        *evb = b & runb;
         ++tail;
         __syncthreads();  // (the shared queue and table written)
         return true;
       };
       if (r == 1) {
         ++nsucc;
-        if (put(t, action, ev1)) first_new = t;
+        if (put(t, action, &evb1)) first_new = t;
       }
       if (crash) {
         ++nsucc;
-        if (put(t2, ACT_CRASH, ev2) && tail0 == tail - 1) first_new = t2;
+        if (put(t2, ACT_CRASH, &evb2) && tail0 == tail - 1) first_new = t2;
       }
       nsucc += (int)uni((uint32_t)selfloop_count_c(L, cu, s));  // Consumer / Terminating stutters
       lvgen += (unsigned)nsucc;
@@ -250,30 +250,24 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       // each component's events: an action error, a deadlock (both the
       // walk's), an invariant of an inserted successor (its own); the rare branch
       const bool walk_ev = (r == 2) | (nsucc == 0 && L.check_deadlock);
-      bool any_ev = false;
-#pragma unroll
-      for (int m = 0; m < M; ++m) any_ev = any_ev | (run(m) & (walk_ev | (ev1[m] != 0) | (ev2[m] != 0)));
-      if (any_ev) {
+      const uint32_t evm = (walk_ev ? runb : 0u) | evb1 | evb2;  // components with an event
+      if (evm) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        if (run(m) && (walk_ev | (ev1[m] != 0) | (ev2[m] != 0))) {
-#pragma nounroll
-          for (int i = 0; i < 2; ++i) {  // an outcome table left it to the programs
-            if ((i ? ev2[m] : ev1[m]) == INV_UNKNOWN + 1) {
-              const int e = check_invariants_direct(L, kc(m), i ? t2 : t) + 1;
-              if (i) ev2[m] = e;
-              else ev1[m] = e;
-            }
-          }
+        if ((evm >> m) & 1u) {
+          // the successors' outcomes, evaluated on the programs (exact, also
+          // where an outcome table left it to them)
+          const int ev1 = (evb1 >> m) & 1u ? check_invariants_direct(L, kc(m), t) + 1 : 0;
+          const int ev2 = (evb2 >> m) & 1u ? check_invariants_direct(L, kc(m), t2) + 1 : 0;
           u64 k = r == 2 ? make_comp_event(level + 1, idx0(m), head, action, EVK_ACTION_ERROR, action)
                   : nsucc == 0 && L.check_deadlock ? make_comp_event(level + 1, idx0(m), head, 15, EVK_DEADLOCK, 0)
                                                    : NO_EVENT;
-          if (ev1[m])
-            k = min(k, make_comp_event(level + 1, idx0(m), head, action, ((ev1[m] - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
-                                       (ev1[m] - 1) >> 1));
-          if (ev2[m])
+          if (ev1)
+            k = min(k, make_comp_event(level + 1, idx0(m), head, action, ((ev1 - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION,
+                                       (ev1 - 1) >> 1));
+          if (ev2)
             k = min(k, make_comp_event(level + 1, idx0(m), head, ACT_CRASH,
-                                       ((ev2[m] - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION, (ev2[m] - 1) >> 1));
+                                       ((ev2 - 1) & 1) ? EVK_INV_ERROR : EVK_VIOLATION, (ev2 - 1) >> 1));
           ev = min(ev, (unsigned long long)k);
           stopb |= (uint32_t)(k != NO_EVENT) << m;
         }
