@@ -81,7 +81,7 @@ COMPONENT_BYTES_PER_STATE = 4  # the per-lane code pass writes one 32-bit record
 # queue position, a walk holding M x 64 components (component.h WAVE_M /
 # WAVE_M_USER, tree.h TREE_WAVE_M), plus, on the tree, each component's walk
 # number and size (2 x 4 B)
-WAVE_M, WAVE_M_USER, TREE_WAVE_M = 10, 4, 8
+WAVE_M, WAVE_M_USER, TREE_WAVE_M = 10, 4, 10
 
 
 def wave_kernel_bytes(comps, m, records, rec_bytes, per_comp=0):

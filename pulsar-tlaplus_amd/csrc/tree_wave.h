@@ -176,12 +176,13 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
           __builtin_amdgcn_raw_buffer_store_b32(key, rr, lane == 0 ? tail * 8 : 0x7fffffff, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b32((uint32_t)head | (uint32_t)ord << 16, rr, lane == 0 ? tail * 8 + 4 : 0x7fffffff,
                                                 0, 0);
+          // each component's invariants: a bit per violating component; its
+          // key (the least is the first component's) only in the rare branch
+          uint32_t vb = 0;
 #pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const int c = check_invariants_cb<W>(L, ccon[m], key);
-            const u64 k = tree_event_key(level + 1, a.comp0 + (b0 + m) * 64 + (u64)lane);
-            evk = in(m) && c >= 0 ? min(evk, k) : evk;
-          }
+          for (int m = 0; m < M; ++m) vb |= (uint32_t)(check_invariants_cb<W>(L, ccon[m], key) >= 0) << m;
+          vb &= inb;
+          if (vb) evk = min(evk, tree_event_key(level + 1, a.comp0 + (b0 + (u64)(__ffs(vb) - 1)) * 64 + (u64)lane));
           ++tail;
           __syncthreads();  // (the shared queue and table written)
           return true;
@@ -197,11 +198,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
         nsucc += (int)uni((uint32_t)selfloop_count_c(L, cu, s));  // Consumer / Terminating stutters
         lvgen += (unsigned)nsucc;
         if (r == 2 || (nsucc == 0 && L.check_deadlock)) {  // an action error or a deadlock: level + 1
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const u64 k = tree_event_key(level + 1, a.comp0 + (b0 + m) * 64 + (u64)lane);
-            evk = in(m) ? min(evk, k) : evk;
-          }
+          if (inb) evk = min(evk, tree_event_key(level + 1, a.comp0 + (b0 + (u64)(__ffs(inb) - 1)) * 64 + (u64)lane));
         }
         ++head;
         cur = head < tail0 ? nxt : first_new;  // position head was filled by this expansion
