@@ -229,8 +229,28 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
         // out of the walk has its outcome masked
         __builtin_amdgcn_raw_buffer_store_b32(comp_record(key, head, act_id), rsrc, lane == 0 ? tail * 4 : 0x7fffffff, 0, 0);
         uint32_t b = 0;
+#ifdef TLCG_USER_INV
 #pragma unroll
         for (int m = 0; m < M; ++m) b |= (uint32_t)(check_invariants_cbt(L, kc(m), key) != -1) << m;
+#else
+        {
+          // the spec's invariants read, besides the code and the walk's Len,
+          // a component's five flags (kf): lane l evaluates them for the flags
+          // l % 32, one ballot gives the outcome of every combination, and
+          // each component reads its own bit -- one evaluation per insert
+          // instead of one per component
+          CodeConsts kl{};
+          kl.len = lenu;
+          kl.msgs_ok = lane & 1;
+          kl.hz_live = (lane >> 1) & 1;
+          kl.hz_false = (lane >> 2) & 1;
+          kl.dn0 = (lane >> 3) & 1;
+          kl.dn1 = (lane >> 4) & 1;
+          const uint32_t vf = (uint32_t)__ballot(check_invariants_cbt(L, kl, key) != -1);
+#pragma unroll
+          for (int m = 0; m < M; ++m) b |= ((vf >> (kf[m] & 31u)) & 1u) << m;
+        }
+#endif
         *evb = b & runb;
         ++tail;
         __syncthreads();  // (the shared queue and table written)

@@ -63,7 +63,13 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
   const u64 nb = (a.n_comp + 63) / 64;
   const int ord_crash = ordinal_of(L, ACT_CRASH, 0);
   for (u64 b0 = (u64)blockIdx.x * M; b0 < nb; b0 += (u64)gridDim.x * M) {
+#ifdef TLCG_USER_INV
     CodeConsts ccon[M];
+#else
+    // the spec's invariants read, besides the code and the walk's Len, five
+    // flags of a component's constants (and its Len: bits 8..): one register
+    uint32_t kf[M];
+#endif
     ckey c0[M];
     uint32_t todob = 0;  // (per component: bit m of a vector register, not a lane mask in scalar registers)
 #pragma unroll
@@ -71,15 +77,26 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       const u64 ci = (b0 + m) * 64 + (u64)lane;
       const bool act = ci < a.n_comp;
       const W s0 = init_state<W>(L, a.comp0 + (act ? ci : 0));
-      ccon[m] = code_consts(L, comp_msgs_init(L, (u64)s0));  // (`messages` sits in the low word)
+      CodeConsts k = code_consts(L, comp_msgs_init(L, (u64)s0));  // (`messages` sits in the low word)
 #ifdef TLCG_USER_INV
-      code_consts_user<W>(L, ccon[m]);  // the user invariants' outcome tables of this component
+      code_consts_user<W>(L, k);  // the user invariants' outcome tables of this component
+      ccon[m] = k;
+#else
+      kf[m] = (uint32_t)(k.msgs_ok != 0) | (uint32_t)(k.hz_live != 0) << 1 | (uint32_t)(k.hz_false != 0) << 2 |
+              (uint32_t)(k.dn0 != 0) << 3 | (uint32_t)(k.dn1 != 0) << 4 | k.len << 8;
 #endif
       c0[m] = code_encode_w<W>(L, s0);
-      const bool ok = act && code_word<W>(L, ccon[m], s0 & messages_mask<W>(L), c0[m]) == s0;
+      const bool ok = act && code_word<W>(L, k, s0 & messages_mask<W>(L), c0[m]) == s0;
       todob |= (uint32_t)ok << m;
       if (act && !ok) flags |= TREE_OVERFLOW;  // no code
     }
+    auto len_of = [&](int m) -> uint32_t {
+#ifdef TLCG_USER_INV
+      return ccon[m].len;
+#else
+      return kf[m] >> 8;
+#endif
+    };
     for (;;) {
       // the walk's leader: the first component still to walk
       int lm = -1;
@@ -93,18 +110,18 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       if (lm < 0) break;
       const int leader = __ffsll((long long)lmask) - 1;
       ckey lc = c0[0];
-      uint32_t ll = ccon[0].len;
+      uint32_t ll = len_of(0);
 #pragma unroll
       for (int m = 1; m < M; ++m)
         if (lm == m) {
           lc = c0[m];
-          ll = ccon[m].len;
+          ll = len_of(m);
         }
       const ckey cu0 = (ckey)__builtin_amdgcn_readlane((int)lc, leader);
       const uint32_t lenu = (uint32_t)__builtin_amdgcn_readlane((int)ll, leader);
       uint32_t inb = 0;
 #pragma unroll
-      for (int m = 0; m < M; ++m) inb |= (uint32_t)(((todob >> m) & 1u) && c0[m] == cu0 && ccon[m].len == lenu) << m;
+      for (int m = 0; m < M; ++m) inb |= (uint32_t)(((todob >> m) & 1u) && c0[m] == cu0 && len_of(m) == lenu) << m;
       todob &= ~inb;
       const int nin = __popc(inb);
       auto in = [&](int m) -> bool { return (inb >> m) & 1u; };
@@ -125,6 +142,29 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
           __builtin_amdgcn_make_buffer_rsrc(a.walk_rec + wid * (u64)CAP, (short)0, CAP * 8, 0x00020000);
       CodeConsts cu{};  // the transitions read Len only
       cu.len = lenu;
+      // bit m: component m's state with code `key` violates an invariant.  The
+      // spec's invariants read the code, the walk's Len and five flags of a
+      // component (kf): lane l evaluates them for the flags l % 32, one ballot
+      // gives every combination's outcome, each component reads its bit
+      auto violators = [&](ckey key) -> uint32_t {
+        uint32_t b = 0;
+#ifdef TLCG_USER_INV
+#pragma unroll
+        for (int m = 0; m < M; ++m) b |= (uint32_t)(check_invariants_cb<W>(L, ccon[m], key) >= 0) << m;
+#else
+        CodeConsts kl{};
+        kl.len = lenu;
+        kl.msgs_ok = lane & 1;
+        kl.hz_live = (lane >> 1) & 1;
+        kl.hz_false = (lane >> 2) & 1;
+        kl.dn0 = (lane >> 3) & 1;
+        kl.dn1 = (lane >> 4) & 1;
+        const uint32_t vf = (uint32_t)__ballot(check_invariants_cb<W>(L, kl, key) >= 0);
+#pragma unroll
+        for (int m = 0; m < M; ++m) b |= ((vf >> (kf[m] & 31u)) & 1u) << m;
+#endif
+        return b & inb;
+      };
       for (int i = lane; i < T; i += 64) h[i] = 0;
       __syncthreads();
       if (lane == 0) {
@@ -134,11 +174,9 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       // position 0: the initial state (no parent)
       __builtin_amdgcn_raw_buffer_store_b32(cu0, rr, lane == 0 ? 0 : 0x7fffffff, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32(0u, rr, lane == 0 ? 4 : 0x7fffffff, 0, 0);
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int c = check_invariants_cb<W>(L, ccon[m], cu0);
-        const u64 k = tree_event_key(0, a.comp0 + (b0 + m) * 64 + (u64)lane);
-        evk = in(m) && c >= 0 ? min(evk, k) : evk;
+      {
+        const uint32_t vb = violators(cu0);
+        if (vb) evk = min(evk, tree_event_key(0, a.comp0 + (b0 + (u64)(__ffs(vb) - 1)) * 64 + (u64)lane));
       }
       __syncthreads();
       int head = 0, tail = 1, level = 0, lvl_start = 0, lvl_end = 1;  // the walk's (scalar)
@@ -178,10 +216,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
                                                 0, 0);
           // each component's invariants: a bit per violating component; its
           // key (the least is the first component's) only in the rare branch
-          uint32_t vb = 0;
-#pragma unroll
-          for (int m = 0; m < M; ++m) vb |= (uint32_t)(check_invariants_cb<W>(L, ccon[m], key) >= 0) << m;
-          vb &= inb;
+          const uint32_t vb = violators(key);
           if (vb) evk = min(evk, tree_event_key(level + 1, a.comp0 + (b0 + (u64)(__ffs(vb) - 1)) * 64 + (u64)lane));
           ++tail;
           __syncthreads();  // (the shared queue and table written)

@@ -105,6 +105,29 @@ def test_tree_error_reported_without_a_global_run(case):
         ck.close()
 
 
+@pytest.mark.parametrize("jit", ["0", "1"])
+@pytest.mark.parametrize("case", ["W_C12_leak", "W_C12_dup"])
+def test_tree_closed_error_reported(case, jit, monkeypatch):
+    """the tree's closed mode (wide components) finds TLC's first error: its
+    least error key names the component, which the host replays in TLC order
+    (verdict, depth, end-of-level counts, trace); TLCG_JIT=1 runs the wave
+    kernel (tree_wave.h), whose violators come from one evaluation per flag
+    combination (a ballot) and whose keys are folded per lane"""
+    monkeypatch.setenv("TLCG_JIT", jit)
+    m = model_of(GOLDEN[case]["constants"])
+    want = GOLDEN[case]["result"]
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run()
+        assert r.engine == "tree" and bool(r.jit_used & 16) == (jit == "1")
+        assert r.status == want["result"] and r.depth == want["depth"]
+        assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+        if "trace" in want:
+            assert [tlcgpu.decode(m, s) for _, s in r.trace] == [t["state"] for t in want["trace"]]
+    finally:
+        ck.close()
+
+
 def test_p8_on_the_tree():
     """~1e8 producer-modelled states (tests/golden/p8.json, from the C oracle)."""
     g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "p8.json")))
