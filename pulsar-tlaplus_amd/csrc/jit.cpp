@@ -59,6 +59,12 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
       i = j + 1;
     }
   }
+  // the big-model wave variant's components per lane and occupancy target:
+  // defined before the headers, whose own defaults (component_wave.h) they
+  // replace (jit_build checks the module's tlcg_wave_m against the host's)
+  if (part == JIT_WAVE_BIG)
+    s += "#ifndef TLCG_WAVE_M\n#define TLCG_WAVE_M " + std::to_string(WAVE_M_BIG) +
+         "\n#endif\n#ifndef TLCG_WAVE_ATTR\n#define TLCG_WAVE_ATTR __attribute__((amdgpu_waves_per_eu(6)))\n#endif\n";
   s += kJitSource;
   s += "\n" + layout_literal(L);
   s += user;
@@ -69,13 +75,19 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
          "{ tlcg::user_check_body<" + w + ">(a, kL); }\n";
     return s;
   }
-  if (part == JIT_WAVE) {
+  if (part == JIT_WAVE || part == JIT_WAVE_BIG) {
+    // the module's components per lane, read back by jit_build: the host's
+    // grid and record tables (crec_index) must use the kernel's M
+    s += "namespace tlcg { extern \"C\" __constant__ int tlcg_wave_m = TLCG_WAVE_M; }\n";
     // the first pass with one walk of the code graph per wave (component_wave.h)
+    // (TLCG_WAVE_ATTR: a tuning hook for the kernels' attributes, e.g. an
+    // occupancy target amdgpu_waves_per_eu; empty by default)
+    s += "#ifndef TLCG_WAVE_ATTR\n#define TLCG_WAVE_ATTR\n#endif\n";
     for (const char* od : {"false", "true"})
-      s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_componentw") +
+      s += std::string("extern \"C\" __global__ __launch_bounds__(64) TLCG_WAVE_ATTR void tlcg_componentw") +
            (od[0] == 't' ? "od" : "") + "_64(tlcg::CompArgs a) { tlcg::component_wave_body<64, " + od + ">(a, kL); }\n";
     // the component tree's closed mode, one walk per wave (tree_wave.h)
-    s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treecw_640(tlcg::TreeArgs a) "
+    s += "extern \"C\" __global__ __launch_bounds__(64) TLCG_WAVE_ATTR void tlcg_treecw_640(tlcg::TreeArgs a) "
          "{ tlcg::tree_wave_body<640, " + w + ">(a, kL); }\n";
     return s;
   }
@@ -114,8 +126,9 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
 // The wave kernels' module (JIT_WAVE) takes the default machine scheduler
 // (TLCG_JIT_OPTS_WAVE): max-ILP measured slower there (G9 1.39-1.41 vs 1.28 ms).
 std::string jit_opts(int part) {
-  const char* e = std::getenv(part == JIT_WAVE ? "TLCG_JIT_OPTS_WAVE" : "TLCG_JIT_OPTS");
-  return e ? e : part == JIT_WAVE ? "" : "-mllvm -amdgpu-sched-strategy=max-ilp";
+  const bool wave = part == JIT_WAVE || part == JIT_WAVE_BIG;
+  const char* e = std::getenv(wave ? "TLCG_JIT_OPTS_WAVE" : "TLCG_JIT_OPTS");
+  return e ? e : wave ? "" : "-mllvm -amdgpu-sched-strategy=max-ilp";
 }
 
 uint64_t fnv1a(const std::string& s) {
@@ -143,7 +156,7 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
   const std::string src = program_source(L, user, part);
   const char* dump_env = std::getenv("TLCG_JIT_DUMP");  // diagnostics: the generated source and code object
   const std::string dump =
-      dump_env ? std::string(dump_env) + (part == JIT_CHECK ? ".check" : part == JIT_WAVE ? ".wave" : "") : "";
+      dump_env ? std::string(dump_env) + (part == JIT_CHECK ? ".check" : part >= JIT_WAVE ? ".wave" : "") : "";
   if (dump_env) {
     std::ofstream f(dump);
     f << src;
@@ -248,15 +261,35 @@ bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStr
   return hipModuleLaunchKernel(k.fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, stream, args, nullptr) == hipSuccess;
 }
 
-bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user) {
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user,
+               uint64_t n_comp) {
+  const bool big = user.empty() && n_comp >= WAVE_BIG_COMPS;
   if (!load_module(L, device, user, JIT_MAIN, &out->module, &out->cached, &out->compile_s, err)) return false;
   bool wcached = false;
   double wcs = 0;
-  if (!load_module(L, device, user, JIT_WAVE, &out->wave_module, &wcached, &wcs, err)) return false;
+  if (!load_module(L, device, user, big ? JIT_WAVE_BIG : JIT_WAVE, &out->wave_module, &wcached, &wcs, err))
+    return false;
   out->compile_s += wcs;
-  out->wave_m = user.empty() ? WAVE_M : WAVE_M_USER;  // (component_wave.h TLCG_WAVE_M)
-  if (const char* d = std::getenv("TLCG_JIT_DEFINES"))  // (a tuning build's own M: the record tables follow it)
-    if (const char* m = std::strstr(d, "TLCG_WAVE_M=")) out->wave_m = std::max(1, std::atoi(m + 12));
+  // the kernel's own M (component_wave.h TLCG_WAVE_M: WAVE_M, WAVE_M_USER,
+  // WAVE_M_BIG, or a tuning define), read from the module: the grid and the
+  // walks' record tables are sized by it
+  {
+    hipDeviceptr_t p = nullptr;
+    size_t n = 0;
+    int m = 0;
+    if (hipModuleGetGlobal(&p, &n, out->wave_module, "tlcg_wave_m") != hipSuccess || n != sizeof(int) ||
+        hipMemcpyDtoH(&m, p, sizeof(int)) != hipSuccess || m < 1 || m > 32) {
+      *err = "the wave module's tlcg_wave_m could not be read";
+      return false;
+    }
+    out->wave_m = m;
+    const int want = big ? WAVE_M_BIG : user.empty() ? WAVE_M : WAVE_M_USER;
+    const char* d = std::getenv("TLCG_JIT_DEFINES");
+    if (m != want && !(d && std::strstr(d, "TLCG_WAVE_M="))) {
+      *err = "the wave module's M (" + std::to_string(m) + ") is not the expected " + std::to_string(want);
+      return false;
+    }
+  }
   if (hipModuleGetFunction(&out->wave[0], out->wave_module, "tlcg_componentw_64") != hipSuccess ||
       hipModuleGetFunction(&out->wave[1], out->wave_module, "tlcg_componentwod_64") != hipSuccess ||
       hipModuleGetFunction(&out->treew, out->wave_module, "tlcg_treecw_640") != hipSuccess) {

@@ -14,7 +14,9 @@
 namespace tlcg {
 
 // the parts of the specialized source (jit.cpp program_source): one module each
-enum JitPart { JIT_MAIN = 0, JIT_CHECK = 1, JIT_WAVE = 2 };
+// JIT_WAVE_BIG: the wave kernels for a model with many components
+// (jit_build: WAVE_M_BIG components per lane at a 6-waves-per-SIMD target)
+enum JitPart { JIT_MAIN = 0, JIT_CHECK = 1, JIT_WAVE = 2, JIT_WAVE_BIG = 3 };
 
 struct JitKernels {
   hipModule_t module = nullptr;
@@ -36,7 +38,11 @@ struct JitKernels {
 // kernels specialized for L on `device`; false with a message on failure.
 // `user`: the model's user invariants as device code (user_device_source),
 // which the kernels then evaluate in the cfg's order with the spec's own.
-bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user = "");
+// n_comp: the components the context's model has (closed partitions: this
+// rank's share), which picks the wave module's variant (JIT_WAVE_BIG from
+// WAVE_BIG_COMPS on, without user invariants)
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user = "",
+               uint64_t n_comp = 0);
 // compile only (no device needed): the code object for `arch`
 // (part: JitPart -- JIT_CHECK the user-check kernel alone, jit_build_user_check; JIT_WAVE the wave kernels)
 bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* code, std::string* err,
