@@ -82,6 +82,7 @@ COMPONENT_BYTES_PER_STATE = 4  # the per-lane code pass writes one 32-bit record
 # WAVE_M_USER, tree.h TREE_WAVE_M), plus, on the tree, each component's walk
 # number and size (2 x 4 B)
 WAVE_M, WAVE_M_USER, TREE_WAVE_M = 10, 4, 10
+WAVE_M_BIG, WAVE_BIG_COMPS = 16, 1 << 23  # (component.h: models with many components)
 
 
 def wave_kernel_bytes(comps, m, records, rec_bytes, per_comp=0):
@@ -550,7 +551,8 @@ def main():
         kt = r["expand_ms"] * 1e-3
         comps = tlcgpu.init_count(model) // world
         wave = bool(r["jit"] & 8)
-        kbytes = wave_kernel_bytes(comps, WAVE_M_USER if cfg.get("user") else WAVE_M, 64, 4) if wave else \
+        wm = WAVE_M_USER if cfg.get("user") else WAVE_M_BIG if comps >= WAVE_BIG_COMPS else WAVE_M
+        kbytes = wave_kernel_bytes(comps, wm, 64, 4) if wave else \
             COMPONENT_BYTES_PER_STATE * distinct / world
         achieved = kbytes / kt / 1e9
         rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
