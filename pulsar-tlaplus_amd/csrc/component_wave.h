@@ -63,7 +63,9 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
   constexpr int T = CodeShape<K>::T;
   constexpr int LV = TLCG_CODE_MAXLV < COMP_MAXLV ? TLCG_CODE_MAXLV : COMP_MAXLV;  // levels tracked
   __shared__ uint16_t q[K];                  // the wave's FIFO of codes
-  __shared__ uint8_t h[T];                   // its FPSet: 1 + queue position, 0 = empty
+  // its FPSet: the code + 1, 0 = empty (a probe is one LDS read instead of a
+  // queue position and then its queue entry; within 1 %, r05_probe_wave_hkey.jsonl)
+  __shared__ uint32_t h[T];
   __shared__ unsigned long long lvl_sh[LV];  // per level: distinct (low 32) + generated (high 32)
   const int lane = threadIdx.x;
   const int mb = L.msg_sh + L.N * L.mw;
@@ -161,7 +163,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
     __syncthreads();  // (the cleared table)
     if (!okm) continue;
     if (lane == 0) {
-      h[slot_of<T>(cu0, a.mult)] = 1;
+      h[slot_of<T>(cu0, a.mult)] = cu0 + 1u;
       q[0] = (uint16_t)cu0;
     }
     u64 lgen = 0;  // successors generated up to the last complete level (the same for every running component)
@@ -217,12 +219,12 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
         unsigned sl = slot_of<T>(key, a.mult);
         unsigned e = h[sl];
         for (int p = 0; uni(e) != 0 && p < T; ++p) {
-          if (uni(q[e - 1] == key ? 1u : 0u)) return false;  // seen
+          if (uni(e == key + 1u ? 1u : 0u)) return false;  // seen
           sl = sl + 1 == (unsigned)T ? 0 : sl + 1;
           e = h[sl];
         }
-        // (every lane writes the same byte: no exec-mask switch)
-        h[sl] = (uint8_t)(tail + 1);
+        // (every lane writes the same word: no exec-mask switch)
+        h[sl] = key + 1u;
         q[tail] = (uint16_t)key;
         // the walk's record of position tail (lane 0), then each running
         // component's invariants, with no branch per component: a component

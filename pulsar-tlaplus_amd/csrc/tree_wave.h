@@ -53,7 +53,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
   constexpr int T = CAP <= 1024 ? 2048 : 4096;  // FPSet slots (load <= 0.31 at CAP 640)
   constexpr int TB = T == 2048 ? 11 : 12;
   __shared__ uint32_t q[CAP];               // the wave's FIFO of codes
-  __shared__ uint16_t h[T];                 // its FPSet: 1 + queue position, 0 = empty
+  __shared__ uint32_t h[T];                 // its FPSet: the code + 1, 0 = empty (a probe is one LDS read)
   __shared__ unsigned long long lvl_d[TREE_MAXLV], lvl_g[TREE_MAXLV];
   const int lane = threadIdx.x;
   for (int i = lane; i < TREE_MAXLV; i += 64) lvl_d[i] = lvl_g[i] = 0;
@@ -168,7 +168,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
       for (int i = lane; i < T; i += 64) h[i] = 0;
       __syncthreads();
       if (lane == 0) {
-        h[(cu0 * 0x9E3779B1u) >> (32 - TB)] = 1;
+        h[(cu0 * 0x9E3779B1u) >> (32 - TB)] = cu0 + 1u;
         q[0] = cu0;
       }
       // position 0: the initial state (no parent)
@@ -200,7 +200,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
           unsigned sl = (key * 0x9E3779B1u) >> (32 - TB);
           unsigned e = h[sl];
           for (int p = 0; uni(e) != 0 && p < T; ++p) {
-            if (uni(q[e - 1] == key ? 1u : 0u)) return false;  // seen
+            if (uni(e == key + 1u ? 1u : 0u)) return false;  // seen
             sl = (sl + 1) & (T - 1);
             e = h[sl];
           }
@@ -208,7 +208,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
             full = true;
             return false;
           }
-          h[sl] = (uint16_t)(tail + 1);
+          h[sl] = key + 1u;
           q[tail] = key;
           // the walk's record of position tail: code, parent position, parent ordinal
           __builtin_amdgcn_raw_buffer_store_b32(key, rr, lane == 0 ? tail * 8 : 0x7fffffff, 0, 0);
