@@ -6,7 +6,16 @@ KeySpace = ValueSpace = {1..15}, MessageSentLimit = 3, CompactionTimesLimit = 3,
 MaxCrashTimes = 1, RetainNullKey, no producer/consumer -> 1,040,187,392
 distinct states, 1,392,508,928 generated, depth 20): FPSet cleared, Init,
 then every BFS level until the queue is empty.  Inputs are the constants;
-everything lives in HBM.  With N GPUs the same job is split across N ranks
+everything lives in HBM.
+
+The headline (`value`, `ms_per_step`, `roofline`) is the fastest engine whose
+timed kernel expands every distinct state: the on-chip engines' per-lane
+kernels (each lane runs its own component's BFS: successors, FPSet probes,
+invariants, store record per state), priced on SURVEY 8(d)'s 34.7 B per
+distinct state.  Beside it: the HBM-FPSet engine (engines.global_hbm_fpset)
+and the one-walk-per-wavefront kernels (engines.wave_quotient), which expand a
+code graph once for M x 64 components -- a product quotient, no roofline.
+With N GPUs the same job is split across N ranks
 (strong scaling): without a Producer each rank runs a contiguous range of the
 components (no data-path collective); the FPSet hash-partitioned by owner
 with the per-level exchange (BASELINE config 4) is measured beside it, and a
@@ -77,19 +86,30 @@ BYTES_PER_STATE_WORD = 8
 # the newest round's profile of each kind (profiles/rNN_*), measured on the same kernels
 PMC_PROFILE = "pmc_k_expand.json"
 COMPONENT_BYTES_PER_STATE = 4  # the per-lane code pass writes one 32-bit record per state (component.h comp_record)
-# the wave kernels (component_wave.h, tree_wave.h) write one record per walk and
-# queue position, a walk holding M x 64 components (component.h WAVE_M /
-# WAVE_M_USER, tree.h TREE_WAVE_M), plus, on the tree, each component's walk
-# number and size (2 x 4 B)
+# the wave kernels (component_wave.h, tree_wave.h) walk a code graph once for
+# M x 64 components (component.h WAVE_M / WAVE_M_USER / WAVE_M_BIG, tree.h TREE_WAVE_M)
 WAVE_M, WAVE_M_USER, TREE_WAVE_M = 10, 4, 10
 WAVE_M_BIG, WAVE_BIG_COMPS = 16, 1 << 23  # (component.h: models with many components)
+# the per-state kernels of the on-chip engines: the one-walk-per-wavefront
+# kernels off (the library's A/B switches)
+PER_STATE_ENV = {"TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "0"}
 
 
-def wave_kernel_bytes(comps, m, records, rec_bytes, per_comp=0):
-    """HBM bytes one wave-kernel launch writes: ceil(ceil(comps / 64) / m)
-    walks x `records` queue positions x rec_bytes, plus per_comp per component"""
-    walks = -(-(-(-comps // 64)) // m)
-    return walks * records * rec_bytes + comps * per_comp
+class per_state_kernels:
+    """the on-chip engines' per-lane kernels for the enclosed runs"""
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in PER_STATE_ENV}
+        os.environ.update(PER_STATE_ENV)
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 MICRO_PROFILE = "profiles/r01_fpset_microbench.jsonl"
 # SURVEY 8(d): algorithmic HBM bytes per distinct state of the BFS path (read
 # the frontier state 8 B, write the new state 8 B and its parent entry 8 B,
@@ -104,9 +124,11 @@ CUS, SIMDS, CLOCK_HZ = 256, 4, 2.4e9
 
 def component_kernel_name(jit):
     """the first-pass component kernel tlcg_stats.jit_used names (bit 0 hipRTC, bit 1 codes,
-    bit 3 one walk of the code graph per wavefront)"""
+    bit 3 one walk of the code graph per wavefront, bit 5 the per-lane bitmap pass)"""
     if jit & 8:
         return "tlcg_componentw_64 (hipRTC-specialized, component codes, one code-graph walk per wavefront)"
+    if jit & 32:
+        return "tlcg_componentp_64 (hipRTC-specialized, component codes, per-lane BFS with a bitmap FPSet)"
     if jit & 1:
         return "tlcg_componentc_64 (hipRTC-specialized, component codes)" if jit & 2 else \
             "tlcg_component_64 (hipRTC-specialized)"
@@ -477,40 +499,55 @@ def main():
                              "(16-B records) + ncclAllReduce per level, RCCL over xGMI")
 
     open_model = bool(cfg.get("producer"))
-    global_run = perlane_run = None
+    global_run = wave_run = None
     if open_model and distributed:
         # the component tree split by subtrees (no exchange), or the level loop's exchange if it hands over
         main_run = time_exchange(0)
     else:
-        main_run = time_engine("auto")
-        global_run = time_engine("global")  # the HBM-FPSet engine beside the on-chip one
-        if main_run["engine"] == "component" and main_run["jit"] & 8:
-            # the component engine's per-lane kernel (component_body.h: every lane
-            # its own FIFO and FPSet) beside the one walk per wavefront
-            os.environ["TLCG_COMP_WAVE"] = "0"
-            try:
-                perlane_run = time_engine("auto")
-            finally:
-                os.environ.pop("TLCG_COMP_WAVE", None)
+        # the headline: the fastest engine whose timed
+        # kernel expands every distinct state -- the on-chip engines' per-lane
+        # kernels (component_body.h: every lane its own component's FIFO,
+        # FPSet probes, invariants; tree_body.h for the closed tree) -- with
+        # the one-walk-per-wavefront kernels switched off
+        with per_state_kernels():
+            main_run = time_engine("auto")
+        if main_run["jit"] & (8 | 16):
+            raise SystemExit("the per-state headline ran a one-walk-per-wavefront kernel")
+        global_run = time_engine("global")  # the HBM-FPSet engine (the north-star design)
+        # the wave kernels (component_wave.h, tree_wave.h): one walk of the code
+        # graph per wavefront applied to M x 64 components -- a product
+        # quotient, reported apart (engines.wave_quotient), never the headline
+        wave_run = time_engine("auto")
+        if not (wave_run["jit"] & (8 | 16)):
+            wave_run = None
     distinct, generated = cfg["distinct"], cfg["generated"]
     # (a producer-modelled cfg has one initial state; its Terminating stutters
     # are not counted out of the probes, so its bytes/state is an upper bound)
     n_init = 1 if open_model else (cfg["keys"] + 1) ** 6
     selfloops = 0 if open_model else n_init * selfloops_per_m(model)
 
+    def survey_roofline(r, kernel):
+        """34.7 algorithmic bytes per distinct state x the distinct
+        states of one step (this rank's share) / the step's kernel time (HIP
+        events around the launches, inside the library) against the 8 TB/s
+        HBM peak -- the same pricing for every per-state engine"""
+        bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
+        kt = r["expand_ms"] * 1e-3
+        achieved = bytes_step / kt / 1e9
+        return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kernel,
+                    launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
+                    bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
+                    algorithmic_bytes_per_step=round(bytes_step),
+                    basis="SURVEY 8(d): read the frontier state 8 B, write the new state 8 B and its parent "
+                          "entry 8 B, g/d = 1.339 FPSet probes of 8 B; x distinct states of one step")
+
     def roofline_global(r):
         abytes = algorithmic_bytes(distinct, generated, n_init, selfloops, words)
-        # SURVEY 8(d)'s per-unit figure x the units (distinct states) of one step, per rank
-        bytes_step = SURVEY_BYTES_PER_DISTINCT * distinct / world
-        achieved = bytes_step / (r["expand_ms"] * 1e-3) / 1e9
-        rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                  kernel=r.get("kernel") or ("k_expand_fast" if words == 1 and not open_model else
-                                             "k_expand_prod<8> (Producer)" if words == 1 else
-                                             "k_expand<u128> (wide FPSet)"),
-                  launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT,
-                  kernel_bytes_per_distinct=round(abytes / distinct, 2))
+        rf = survey_roofline(r, r.get("kernel") or ("k_expand_fast" if words == 1 and not open_model else
+                                                    "k_expand_prod<8> (Producer)" if words == 1 else
+                                                    "k_expand<u128> (wide FPSet)"))
+        rf["kernel_bytes_per_distinct"] = round(abytes / distinct, 2)
         new = pmc_fields(f"expand_{args.config}", rf["kernel"], r["expand_ms"] * 1e-3, distinct) \
             if world == 1 and words == 1 and not open_model else None
         if new:
@@ -534,39 +571,17 @@ def main():
                 frac=round(bound_ms / r["expand_ms"], 3), source=MICRO_PROFILE)
         return rf
 
-    def survey_equivalent(r):
-        """SURVEY 8(d)'s 34.7 B per distinct state (the HBM-FPSet design's bytes)
-        at this run's speed: a notional rate, not the kernel's traffic"""
-        gbs = SURVEY_BYTES_PER_DISTINCT * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
-        return dict(bytes_per_distinct=SURVEY_BYTES_PER_DISTINCT, gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4),
-                    note="notional: the on-chip engines keep their FPSet and FIFO in LDS and never move these bytes")
+    ON_CHIP_NOTE = ("on-chip engine: each lane expands its own component's states with its FIFO and FPSet in "
+                    "LDS, so SURVEY 8(d)'s bytes move through LDS, not HBM (roofline.traffic is the HBM the "
+                    "kernel did move, by PMC); roofline.issue is the bound that binds it (DESIGN 4)")
 
     def roofline_component(r):
-        # the kernel's own algorithmic HBM bytes: the per-lane kernel writes
-        # one 4-B record per distinct state (comp_record; its FIFO and FPSet
-        # stay in LDS, the components' constants come from the initial-state
-        # index; the 32-bit cascade passes, none on G9, write 16 B); the wave
-        # kernel one record per walk and queue position (K = 64); SURVEY
-        # 8(d)'s 34.7 B/state (the HBM-FPSet design's) beside it as survey_equivalent
+        # the per-lane kernel: its own HBM bytes are one 4-B store record per
+        # distinct state (comp_record; FIFO and FPSet in LDS)
         kt = r["expand_ms"] * 1e-3
-        comps = tlcgpu.init_count(model) // world
-        wave = bool(r["jit"] & 8)
-        wm = WAVE_M_USER if cfg.get("user") else WAVE_M_BIG if comps >= WAVE_BIG_COMPS else WAVE_M
-        kbytes = wave_kernel_bytes(comps, wm, 64, 4) if wave else \
-            COMPONENT_BYTES_PER_STATE * distinct / world
-        achieved = kbytes / kt / 1e9
-        rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                  kernel=component_kernel_name(r["jit"]),
-                  launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=round(kbytes * world / distinct, 4),
-                  bytes_basis="the kernel's HBM bytes per distinct state: " +
-                              ("one 4-B record per walk and queue position, a walk serving M x 64 components; the "
-                               "binding resource is the walk's issue (roofline.issue), not HBM (DESIGN 4)" if wave else
-                               "its 4-B store record (DESIGN 4)"),
-                  survey_equivalent=survey_equivalent(r))
-        # (each kernel priced with its own profile: component_<cfg> = the one walk per
-        # wavefront, component_perlane_<cfg> = component_body.h's lanes)
+        rf = survey_roofline(r, component_kernel_name(r["jit"]))
+        rf["kernel_hbm_bytes_per_distinct"] = COMPONENT_BYTES_PER_STATE
+        rf["note"] = ON_CHIP_NOTE
         new = None
         if world == 1:
             for prof in ([f"component_{args.config}"] if r["jit"] & 8 else
@@ -574,38 +589,30 @@ def main():
                 new = new or pmc_fields(prof, rf["kernel"], kt, distinct)
         if new:
             rf.update(new)
-            rf["traffic_over_algorithmic"] = round(new["traffic_bytes_per_step"] / kbytes, 3)
+            rf["traffic_over_kernel_bytes"] = round(new["traffic_bytes_per_step"] /
+                                                    (COMPONENT_BYTES_PER_STATE * distinct / world), 3)
         return rf
 
-    def roofline_tree(r):
-        # SURVEY 8(d)'s per-unit figure x the distinct states of one step; the
-        # kernel writes the parent entry per state and the state word (Producer
-        # modelled, plus a depth byte the next layer reads with the parent
-        # state, 9 B per entry) or, closed, the 4-B component code the host
-        # decodes (tree_body.h TLCG_TREE_CODE_STORE); its FPSets stay in LDS
-        per_state = BYTES_PER_STATE_WORD * (words + 1) + 1 if open_model else 4 + BYTES_PER_STATE_WORD
-        if r["jit"] & 16:  # the closed wave kernel: 8-B records per walk and position, 8 B per component
-            per_state = wave_kernel_bytes(tlcgpu.init_count(model) // world, TREE_WAVE_M, 640, 8, 8) * world / distinct
-        achieved = per_state * distinct / world / (r["expand_ms"] * 1e-3) / 1e9
+    def tree_kernel_name(jit):
         if open_model:
-            kern = ("tlcg_tree_384 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<384, 512, 4> (") + \
+            return ("tlcg_tree_384 (hipRTC-specialized, " if jit & 1 else "k_tree<384, 512, 4> (") + \
                 "component tree, 4 components per wavefront)"
-        else:
-            kern = "tlcg_treecw_640 (hipRTC-specialized, component tree closed mode: component codes, one " \
-                "code-graph walk per wavefront, lane-interleaved store)" if r["jit"] & 16 else \
-                ("tlcg_treec_640 (hipRTC-specialized, " if r["jit"] & 1 else "k_tree<640, 1024, 4, closed> (") + \
-                "component tree closed mode: component codes, 4 components per wavefront)"
-        rf = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                  frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kern,
-                  launches_per_step=r["launches"], avg_launch_ms=round(r["expand_ms"] / r["launches"], 4),
-                  bytes_per_distinct=round(per_state, 4),
-                  bytes_basis="the kernel's HBM bytes per distinct state: " +
-                              ("its walks' 8-B records (one per walk and queue position, a walk serving M x 64 "
-                               "components) and each component's walk and size; the binding resource is the walk's "
-                               "issue (roofline.issue), not HBM (DESIGN 4)" if r["jit"] & 16 else
-                               "the stored state or code and its parent reference (DESIGN 4)"),
-                  survey_equivalent=survey_equivalent(r))
-        new = pmc_fields(f"tree_{args.config}", kern, r["expand_ms"] * 1e-3, distinct) if world == 1 else None
+        if jit & 16:
+            return "tlcg_treecw_640 (hipRTC-specialized, component tree closed mode: one code-graph walk " \
+                "per wavefront, lane-interleaved store)"
+        return ("tlcg_treec_640 (hipRTC-specialized, " if jit & 1 else "k_tree<640, 1024, 4, closed> (") + \
+            "component tree closed mode: component codes, 4 components per wavefront)"
+
+    def roofline_tree(r):
+        # the tree writes the parent entry per state and the state word
+        # (Producer modelled, plus a depth byte: 9 B per entry) or, closed, the
+        # 4-B component code the host decodes; its FPSets stay in LDS
+        rf = survey_roofline(r, tree_kernel_name(r["jit"]))
+        rf["kernel_hbm_bytes_per_distinct"] = BYTES_PER_STATE_WORD * (words + 1) + 1 if open_model else \
+            4 + BYTES_PER_STATE_WORD
+        rf["note"] = ON_CHIP_NOTE
+        prof = f"tree_{args.config}" if open_model else f"tree_perlane_{args.config}"
+        new = pmc_fields(prof, rf["kernel"], r["expand_ms"] * 1e-3, distinct) if world == 1 else None
         if new:
             rf.update(new)
         return rf
@@ -620,6 +627,33 @@ def main():
             if k in r:
                 out[k] = r[k]
         return out
+
+    def wave_summary(r):
+        """the one-walk-per-wavefront kernels: a wave expands its code graph
+        once (the code states of one component) and applies each expansion to
+        the M x 64 components of the walk (their invariants by one ballot over
+        the 32 flag combinations, component_wave.h) -- a quotient of the product
+        state space, not a per-state throughput: no roofline is claimed"""
+        comps = tlcgpu.init_count(model) // world
+        per_comp = distinct // (cfg["keys"] + 1) ** 6 if not open_model else None
+        if r["engine"] == "tree":
+            m, kern = TREE_WAVE_M, tree_kernel_name(r["jit"])
+        else:
+            m = WAVE_M_USER if cfg.get("user") else WAVE_M_BIG if comps >= WAVE_BIG_COMPS else WAVE_M
+            kern = component_kernel_name(r["jit"])
+        walks = -(-(-(-comps // 64)) // m)
+        expanded = walks * per_comp if per_comp else None
+        return dict(engine=r["engine"], kernel=kern, quotient=True,
+                    value_quotient=round(distinct * args.steps / r["elapsed"], 1),
+                    ms_per_step=round(r["elapsed"] * 1e3 / args.steps, 3),
+                    gpu_kernel_ms_per_step=round(r["kernel_ms"], 3),
+                    components_per_walk=m * 64, walks_per_step=walks,
+                    code_states_expanded=expanded,
+                    states_per_expansion=round(distinct / world / expanded, 1) if expanded else None,
+                    roofline=None,
+                    note="a product quotient (messages is immutable and the code transitions read only Len): "
+                         "the rate grows with components per walk, not with hardware throughput; not a "
+                         "per-state BFS rate (VERDICT r5)")
 
     main_s = summary(main_run)
 
@@ -653,8 +687,8 @@ def main():
             line["config"]["user_invariants"] = {n: USER_DEFS[n] for n in user_invariants(args.config)}
         if global_run:
             line["engines"]["global_hbm_fpset"] = summary(global_run)
-        if perlane_run:
-            line["engines"]["component_per_lane"] = summary(perlane_run)
+        if wave_run:
+            line["engines"]["wave_quotient"] = wave_summary(wave_run)
         if distributed:
             line["dist_backend"] = args.dist_backend
             line["rccl_ranks"] = preflight["rccl_ranks"] if preflight else None

@@ -171,7 +171,10 @@ typedef struct tlcg_stats {
                                 bit 3: the code pass walked each code graph once per wavefront
                                 for its components (tlcg_componentw_64, component_wave.h);
                                 bit 4: the component tree's closed mode did the same
-                                (tlcg_treecw_640, tree_wave.h: its store is lane-interleaved) */
+                                (tlcg_treecw_640, tree_wave.h: its store is lane-interleaved);
+                                bit 5: the code pass ran per lane with a bitmap FPSet over a slot
+                                hash injective on the component code set (tlcg_componentp_64,
+                                component_lane.h) */
   uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
   uint64_t fpset_host_states; /* states held by the host FPSet tier (tlcg_opts.fpset_spill) */
   uint64_t transport;        /* multi-rank runs: 1 host threads + device copies, 2 RCCL; 0 one context */

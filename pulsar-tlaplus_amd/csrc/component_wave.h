@@ -138,7 +138,13 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const bool act = (b0 + m) * 64 + (u64)lane < a.n_comp;
+#ifndef TLCG_WAVE_REFUSE_ODD
       const bool r = code_ok[m] && c0[m] == cu0 && ccon[m].len == lenu;
+#else
+      // (test hook: the components of odd batch + lane parity refuse the walk,
+      // so the fallback below and the cascade pass run; tests/test_gpu_wave_parity.py)
+      const bool r = code_ok[m] && c0[m] == cu0 && ccon[m].len == lenu && (((b0 + (u64)m) ^ (u64)lane) & 1) == 0;
+#endif
       runb |= (uint32_t)r << m;
       if (act && !r) a.ovf_list[atomicAdd(a.ovf_n, 1ull)] = idx0(m);
     }

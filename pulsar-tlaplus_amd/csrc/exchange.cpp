@@ -162,7 +162,15 @@ class RcclTransport : public Transport {
     return nccl(R()->GroupEnd(), "ncclGroupEnd", err) && (!wait_done || wait(err));
   }
 
-  bool can_pipeline() const override { return true; }
+  // the one-wait level over RCCL is opt-in (TLCG_PIPELINE=1): no run of more
+  // than one RCCL rank has recorded its counts and timeline yet, and its one
+  // wait bounds the level's kernels as well as the collective under
+  // TLCG_COMM_TIMEOUT_S; the default is the two-step level, whose
+  // wait covers the send/recv alone
+  bool can_pipeline() const override {
+    const char* v = std::getenv("TLCG_PIPELINE");
+    return v && !std::strcmp(v, "1");
+  }
   bool wait_stream(tlcg_ctx*, std::string* err) override { return wait(err); }
 
   bool allreduce(uint64_t* v, int n, RedOp op, std::string* err) override {

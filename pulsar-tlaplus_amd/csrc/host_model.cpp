@@ -2,6 +2,7 @@
 // model-level (context-free) C-ABI entry points.
 #include "host_model.h"
 
+#include "component.h"
 #include "component_code.h"
 #include "component_model.h"
 
@@ -304,6 +305,39 @@ bool build_slot_disp(const HostModel& hm, int T, uint32_t mult, uint32_t* dmult,
     if (ok) {
       *dmult = dm;
       std::copy(d, d + NB, disp);
+      return true;
+    }
+  }
+  return false;
+}
+
+bool build_lane_phash(const HostModel& hm, uint32_t* mult, uint32_t* owner) {
+  std::fill(owner, owner + LANE_T, 0u);
+  *mult = 0;
+  if (hm.L.producer || code_bits(hm.L) > 16) return false;
+  std::vector<std::vector<uint32_t>> calls;
+  std::vector<uint32_t> codes;
+  if (!comp0_calls(hm, 63, 1, &calls, &codes)) return false;  // (>= 63 states: past the pass's K = 64 - 2)
+  std::vector<uint32_t> used(LANE_T, 0);
+  uint64_t x = 0x2545F4914F6CDD1Dull;  // a fixed sequence: the choice is deterministic
+  for (int i = 0; i < (1 << 20); ++i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    const uint32_t m = ((uint32_t)(x >> 20) & 0xFFFFFFu) | 1u;
+    std::fill(used.begin(), used.end(), 0u);
+    bool ok = true;
+    for (uint32_t c : codes) {
+      const unsigned sl = lane_slot(c, m);
+      if (used[sl]) {
+        ok = false;
+        break;
+      }
+      used[sl] = c + 1u;
+    }
+    if (ok) {
+      *mult = m;
+      std::copy(used.begin(), used.end(), owner);
       return true;
     }
   }

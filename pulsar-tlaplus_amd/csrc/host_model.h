@@ -61,6 +61,14 @@ uint32_t tune_slot_mult(const HostModel& hm, int T, int group, int candidates);
 // no table was found (then `disp` is all zero).
 bool build_slot_disp(const HostModel& hm, int T, uint32_t mult, uint32_t* dmult, uint16_t* disp);
 
+// the per-lane bitmap pass (component_lane.h): a 24-bit multiplier under
+// which lane_slot (the top 8 bits of code x mult) is injective on component
+// 0's code set -- without a Producer the code set every component shares --
+// and owner[s] = the code in slot s + 1 (0: none), LANE_T entries.  The first
+// multiplier of a fixed sequence that works; false when the component has 63
+// or more states (the pass's capacity) or no multiplier was found
+bool build_lane_phash(const HostModel& hm, uint32_t* mult, uint32_t* owner);
+
 // every invariant of the cfg, the user's included: -1, else (index << 1) | is_error
 template <typename W>
 int host_check_all(const HostModel& hm, W s) {

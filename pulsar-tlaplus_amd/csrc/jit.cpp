@@ -101,6 +101,10 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
              "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ", " + od + ", " + code +
              ">(a, kL); }\n";
       }
+  // the per-lane code pass with a bitmap FPSet (component_lane.h)
+  for (const char* od : {"false", "true"})
+    s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_componentp") +
+         (od[0] == 't' ? "od" : "") + "_64(tlcg::CompArgs a) { tlcg::component_lane_body<64, " + od + ">(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_384(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_1024(tlcg::TreeArgs a) "
@@ -261,10 +265,12 @@ bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStr
   return hipModuleLaunchKernel(k.fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, stream, args, nullptr) == hipSuccess;
 }
 
-bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user,
-               uint64_t n_comp) {
-  const bool big = user.empty() && n_comp >= WAVE_BIG_COMPS;
-  if (!load_module(L, device, user, JIT_MAIN, &out->module, &out->cached, &out->compile_s, err)) return false;
+namespace {
+
+// the wave module (JIT_WAVE / JIT_WAVE_BIG): loaded, its tlcg_wave_m read
+// back and checked, its kernels looked up; false with a message otherwise
+bool load_wave_module(const Layout& L, int device, const std::string& user, bool big, JitKernels* out,
+                      std::string* err) {
   bool wcached = false;
   double wcs = 0;
   if (!load_module(L, device, user, big ? JIT_WAVE_BIG : JIT_WAVE, &out->wave_module, &wcached, &wcs, err))
@@ -273,27 +279,50 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
   // the kernel's own M (component_wave.h TLCG_WAVE_M: WAVE_M, WAVE_M_USER,
   // WAVE_M_BIG, or a tuning define), read from the module: the grid and the
   // walks' record tables are sized by it
-  {
-    hipDeviceptr_t p = nullptr;
-    size_t n = 0;
-    int m = 0;
-    if (hipModuleGetGlobal(&p, &n, out->wave_module, "tlcg_wave_m") != hipSuccess || n != sizeof(int) ||
-        hipMemcpyDtoH(&m, p, sizeof(int)) != hipSuccess || m < 1 || m > 32) {
-      *err = "the wave module's tlcg_wave_m could not be read";
-      return false;
-    }
-    out->wave_m = m;
-    const int want = big ? WAVE_M_BIG : user.empty() ? WAVE_M : WAVE_M_USER;
-    const char* d = std::getenv("TLCG_JIT_DEFINES");
-    if (m != want && !(d && std::strstr(d, "TLCG_WAVE_M="))) {
-      *err = "the wave module's M (" + std::to_string(m) + ") is not the expected " + std::to_string(want);
-      return false;
-    }
+  hipDeviceptr_t p = nullptr;
+  size_t n = 0;
+  int m = 0;
+  if (hipModuleGetGlobal(&p, &n, out->wave_module, "tlcg_wave_m") != hipSuccess || n != sizeof(int) ||
+      hipMemcpyDtoH(&m, p, sizeof(int)) != hipSuccess || m < 1 || m > 32) {
+    *err = "the wave module's tlcg_wave_m could not be read";
+    return false;
   }
+  const int want = big ? WAVE_M_BIG : user.empty() ? WAVE_M : WAVE_M_USER;
+  const char* d = std::getenv("TLCG_JIT_DEFINES");
+  if (m != want && !(d && std::strstr(d, "TLCG_WAVE_M="))) {
+    *err = "the wave module's M (" + std::to_string(m) + ") is not the expected " + std::to_string(want);
+    return false;
+  }
+  out->wave_m = m;
   if (hipModuleGetFunction(&out->wave[0], out->wave_module, "tlcg_componentw_64") != hipSuccess ||
       hipModuleGetFunction(&out->wave[1], out->wave_module, "tlcg_componentwod_64") != hipSuccess ||
       hipModuleGetFunction(&out->treew, out->wave_module, "tlcg_treecw_640") != hipSuccess) {
     *err = "hipModuleGetFunction tlcg_componentw_64 / tlcg_treecw_640";
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, const std::string& user,
+               uint64_t n_comp) {
+  const bool big = user.empty() && n_comp >= wave_big_comps();
+  if (!load_module(L, device, user, JIT_MAIN, &out->module, &out->cached, &out->compile_s, err)) return false;
+  // the wave kernels are optional: a module that fails to build,
+  // load or check leaves them unset -- the first passes then run the per-lane
+  // kernels (run_component, run_tree) -- and its message in wave_error
+  std::string werr;
+  if (!load_wave_module(L, device, user, big, out, &werr)) {
+    out->wave_error = werr.empty() ? "the wave module failed" : werr;
+    if (out->wave_module) hipModuleUnload(out->wave_module);
+    out->wave_module = nullptr;
+    out->wave[0] = out->wave[1] = out->treew = nullptr;
+    out->wave_m = WAVE_M;
+  }
+  if (hipModuleGetFunction(&out->lane[0], out->module, "tlcg_componentp_64") != hipSuccess ||
+      hipModuleGetFunction(&out->lane[1], out->module, "tlcg_componentpod_64") != hipSuccess) {
+    *err = "hipModuleGetFunction tlcg_componentp_64";
     return false;
   }
   const char* names[4] = {"32", "64", "128", "255"};
@@ -328,13 +357,16 @@ void jit_release(JitKernels* k) {
   if (k) *k = JitKernels();
 }
 
-bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream, bool wave) {
+bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream, bool wave,
+                          bool lane) {
   if (!a.n_comp) return true;
   const int i = K == 32 ? 0 : K == 64 ? 1 : K == 128 ? 2 : 3;
   hipFunction_t f = a.outdeg ? k.component_od[i] : k.component[i];
   if (code && i < 2) f = a.outdeg ? k.code_od[i] : k.code[i];
   const bool w = wave && code && K == 64;
   if (w) f = a.outdeg ? k.wave[1] : k.wave[0];
+  if (!w && lane && code && K == 64) f = a.outdeg ? k.lane[1] : k.lane[0];
+  if (!f) return false;
   const uint64_t batches = w ? (a.n_comp + 64 * (u64)k.wave_m - 1) / (64 * (u64)k.wave_m) : (a.n_comp + 63) / 64;
   const unsigned grid = (unsigned)(batches < comp_grid_cap() ? batches : comp_grid_cap());
   CompArgs copy = a;

@@ -27,7 +27,9 @@ struct JitKernels {
   hipFunction_t code_od[2] = {nullptr, nullptr};
   hipFunction_t wave[2] = {nullptr, nullptr};     // codes, K = 64, one walk per wave (component_wave.h); outdegrees
   hipFunction_t treew = nullptr;                  // the tree's closed mode at 640 states, one walk per wave (tree_wave.h)
+  hipFunction_t lane[2] = {nullptr, nullptr};     // codes, K = 64, per lane with a bitmap FPSet (component_lane.h); outdegrees
   int wave_m = WAVE_M;                            // its components per lane (the grid)
+  std::string wave_error;                         // why the wave kernels are unset (jit_build), else empty
   hipFunction_t tree[4] = {nullptr, nullptr, nullptr, nullptr};  // component tree: 384 x 4 groups, 1024 x 1;
                                                                  // closed mode: 640 x 4, 2048 x 1
   double compile_s = 0;  // 0 when loaded from the cache
@@ -49,8 +51,9 @@ bool jit_compile(const Layout& L, const std::string& arch, std::vector<char>* co
                  const std::string& user = "", int part = JIT_MAIN);
 void jit_release(JitKernels* k);
 // (wave: the first pass's kernel with one walk of the code graph per wave, component_wave.h)
+// (lane: the per-lane code pass with a bitmap FPSet, component_lane.h)
 bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool code, hipStream_t stream,
-                          bool wave = false);
+                          bool wave = false, bool lane = false);
 // the global engine's user-invariant check (kernels.h user_check_body) as
 // device code: a module of its own, so a global-engine check does not wait
 // for the on-chip engines' kernels to compile
