@@ -435,6 +435,10 @@ def main():
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
         counts = [st.generated, st.distinct]
+        try:  # the kernels' own count of state expansions (tlcg_expansions)
+            expansions = eng.ck.expansions()
+        except RuntimeError:
+            expansions = None
         used = tlcgpu.ENGINE_NAMES.get(int(st.engine), "?")
         jit = int(st.jit_used)
         launches = len(eng.level_sizes()) if used == "global" else \
@@ -443,6 +447,13 @@ def main():
             t = torch.tensor([elapsed, ems, kms], dtype=torch.float64, device=rdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed, ems, kms = [float(x) for x in t.tolist()]
+            x = torch.tensor([expansions if expansions is not None else -1], dtype=torch.int64, device=rdev)
+            dist.all_reduce(x, op=dist.ReduceOp.MIN)
+            if int(x.item()) >= 0:
+                dist.all_reduce(x.fill_(expansions), op=dist.ReduceOp.SUM)
+                expansions = int(x.item())
+            else:
+                expansions = None
             c = torch.tensor(counts, dtype=torch.int64, device=rdev)
             dist.all_reduce(c, op=dist.ReduceOp.SUM)
             counts = [int(x) for x in c.tolist()]
@@ -450,7 +461,7 @@ def main():
         if tuple(counts) != (cfg["generated"], cfg["distinct"]):
             raise SystemExit(f"count mismatch ({engine}): {counts} want {cfg}")
         return dict(engine=used, jit=jit, elapsed=elapsed, expand_ms=ems / args.steps, kernel_ms=kms / args.steps,
-                    launches=launches)
+                    launches=launches, expansions=expansions)
 
     def time_exchange(partition):
         """The global engine with successors crossing ranks, so every BFS level
@@ -623,6 +634,11 @@ def main():
                    gpu_kernel_ms_per_step=round(r["kernel_ms"], 3),
                    roofline=roofline_component(r) if r["engine"] == "component" else
                    roofline_tree(r) if r["engine"] == "tree" else roofline_global(r))
+        if r.get("expansions") is not None:
+            # the kernels' own count (tlcg_expansions): every distinct state
+            # expanded once by a per-state kernel
+            out["expansions_per_step"] = r["expansions"]
+            out["distinct_per_expansion"] = round(distinct / max(r["expansions"], 1), 3)
         for k in ("partition", "exchange"):
             if k in r:
                 out[k] = r[k]
@@ -642,7 +658,8 @@ def main():
             m = WAVE_M_USER if cfg.get("user") else WAVE_M_BIG if comps >= WAVE_BIG_COMPS else WAVE_M
             kern = component_kernel_name(r["jit"])
         walks = -(-(-(-comps // 64)) // m)
-        expanded = walks * per_comp if per_comp else None
+        # the kernel's own count (tlcg_expansions: one per walk and code state)
+        expanded = r.get("expansions") or (walks * per_comp if per_comp else None)
         return dict(engine=r["engine"], kernel=kern, quotient=True,
                     value_quotient=round(distinct * args.steps / r["elapsed"], 1),
                     ms_per_step=round(r["elapsed"] * 1e3 / args.steps, 3),
@@ -656,6 +673,8 @@ def main():
                          "per-state BFS rate (VERDICT r5)")
 
     main_s = summary(main_run)
+    if main_s.get("expansions_per_step") is not None:
+        main_s["roofline"]["expansions_per_step"] = main_s["expansions_per_step"]
 
     def build_line(exchange_run, exchange_error):
         line = {
@@ -682,6 +701,9 @@ def main():
             "roofline": main_s["roofline"],
             "engines": {},
         }
+        if main_s.get("expansions_per_step") is not None:
+            line["expansions_per_step"] = main_s["expansions_per_step"]
+            line["distinct_per_expansion"] = main_s["distinct_per_expansion"]
         if user_invariants(args.config):
             line["config"]["invariants"] = list(model.invariants)
             line["config"]["user_invariants"] = {n: USER_DEFS[n] for n in user_invariants(args.config)}

@@ -242,6 +242,16 @@ int tlcg_tlc_stop_stats(tlcg_ctx* c, uint64_t* generated, uint64_t* distinct, ui
  * parents: a global-engine run in TLC order (world 1) or the component
  * engine; refused otherwise, and after tlcg_recover.  [TLC-ext] */
 int tlcg_outdegree(tlcg_ctx* c, uint64_t* hist, int32_t cap, int32_t* n);
+/* State expansions the last check's kernels made (*out): the component
+ * engine counts, per pass, the states expanded for the components that finish
+ * in it -- each state of each component for a per-lane kernel
+ * (component_body.h, component_lane.h), each code state of a walk once for all
+ * the walk's M x 64 components for the one-walk-per-wavefront kernel
+ * (component_wave.h); the one-rank global engine reports the states of its
+ * expanded levels.  So distinct / expansions is 1 for a per-state kernel and
+ * the components per walk for the wave kernel.  -2 for other engines.  (TLC
+ * has no counterpart: its workers expand each state once.) */
+int tlcg_expansions(tlcg_ctx* c, uint64_t* out);
 /* States generated per BFS level: out[0] = the initial states, out[k] = the
  * successors generated by expanding level k - 1 (stutters included), *n =
  * expanded levels + 1.  The sum is tlcg_stats.generated; the sum of

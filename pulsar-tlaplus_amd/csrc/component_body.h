@@ -169,6 +169,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
   const int mb = L.msg_sh + L.N * L.mw;  // `messages` occupies the low mb bits
   if (lane < LV) lvl_sh[lane] = 0;
   u64 gen = 0, dist = 0;
+  uint32_t nexp = 0;  // states expanded (of the components that finish here)
   unsigned od0 = 0, od1 = 0, od2 = 0;  // TLC's outdegree histogram: states with 0 / 1 / 2 new successors
   unsigned long long ev = NO_EVENT;
   __syncthreads();
@@ -567,6 +568,7 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
       if (tail > lvl_start && level >= counted) atomicAdd(&lvl_sh[level], (unsigned long long)(tail - lvl_start));
       gen += lgen;
       dist += (u64)tail;
+      nexp += (uint32_t)head;
       if constexpr (OD) {
         od0 += ocnt & 1023;
         od1 += (ocnt >> 10) & 1023;
@@ -577,12 +579,14 @@ __device__ __forceinline__ void component_body(const CompArgs& a, const Layout& 
   }
   gen = wave_sum_u64(gen);
   dist = wave_sum_u64(dist);
+  const u64 nx = wave_sum_u64(nexp);
   const u64 o0 = wave_sum_u64(od0), o1 = wave_sum_u64(od1), o2 = wave_sum_u64(od2);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) ev = min(ev, (unsigned long long)__shfl_xor(ev, off));
   __syncthreads();
   const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy
   if (lane == 0) {
+    if (nx && a.expansions) atomicAdd(&a.expansions[so], (unsigned long long)nx);
     if (gen) atomicAdd(&a.totals[so + 0], (unsigned long long)gen);
     if (dist) atomicAdd(&a.totals[so + 1], (unsigned long long)dist);
     if (ev != NO_EVENT) atomicMin(a.event, ev);

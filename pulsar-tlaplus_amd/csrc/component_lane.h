@@ -70,7 +70,7 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
   const uint32_t mult = a.lane_mult;
   for (int i = lane; i < T; i += 64) owner[i] = a.lane_owner[i];
   if (lane < LV) lvl_sh[lane] = 0;
-  uint32_t gen = 0, dist = 0;
+  uint32_t gen = 0, dist = 0, nexp = 0;  // (nexp: states expanded by the components that finish here)
   unsigned od0 = 0, od1 = 0, od2 = 0;
   unsigned long long ev = NO_EVENT;
   __syncthreads();
@@ -164,11 +164,13 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
       // read) and each new state's record at its position
       ring[tail & (R - 1)][lane] = (uint16_t)t;
       ring[(tail + (new1 ? 1 : 0)) & (R - 1)][lane] = (uint16_t)t2;
+#ifndef TLCG_NO_STORE  // (experiment only: measures what the records cost)
       __builtin_amdgcn_raw_buffer_store_b32(comp_record(t, head, action), rsrc,
                                             new1 ? (int)((unsigned)tail * 256u + loff) : OOB, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32(comp_record(t2, head, ACT_CRASH), rsrc,
                                             new2 ? (int)((unsigned)(tail + (new1 ? 1 : 0)) * 256u + loff) : OOB, 0,
                                             0);
+#endif
       const ckey first_new = new1 ? t : t2;
       tail += (new1 ? 1 : 0) + (new2 ? 1 : 0);
       const int nsucc = (e1 ? 1 : 0) + (e2 ? 1 : 0) + (alive ? selfloop_count_c(L, ccon, s) : 0);  // + stutters
@@ -176,8 +178,12 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
       if constexpr (OD) ocnt += alive ? 1u << (10 * (tail - tail0)) : 0u;  // new states this expansion discovered
       // the inserted successors' invariants (first failing + 1; INV_UNKNOWN
       // + 1: an outcome table left it to the programs, the rare branch)
+#ifndef TLCG_NO_INV  // (experiment only: measures what the invariants cost)
       int ev1 = new1 ? check_invariants_cbt(L, ccon, t) + 1 : 0;
       int ev2 = new2 ? check_invariants_cbt(L, ccon, t2) + 1 : 0;
+#else
+      int ev1 = 0, ev2 = 0;
+#endif
       // an action error (no successor from the failing action; the others
       // still count, as k_expand), a deadlock and the successors' invariant
       // events in one rare branch
@@ -241,6 +247,7 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
     if (fin) {
       gen += lgen;
       dist += (uint32_t)tail;
+      nexp += (uint32_t)head;
       if constexpr (OD) {
         od0 += ocnt & 1023;
         od1 += (ocnt >> 10) & 1023;
@@ -249,13 +256,14 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
       ev = min(ev, (unsigned long long)lev);
     }
   }
-  const u64 g64 = wave_sum_u64(gen), d64 = wave_sum_u64(dist);
+  const u64 g64 = wave_sum_u64(gen), d64 = wave_sum_u64(dist), x64 = wave_sum_u64(nexp);
   const u64 o0 = wave_sum_u64(od0), o1 = wave_sum_u64(od1), o2 = wave_sum_u64(od2);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) ev = min(ev, (unsigned long long)__shfl_xor(ev, off));
   __syncthreads();
   const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy
   if (lane == 0) {
+    if (x64 && a.expansions) atomicAdd(&a.expansions[so], (unsigned long long)x64);
     if (g64) atomicAdd(&a.totals[so + 0], (unsigned long long)g64);
     if (d64) atomicAdd(&a.totals[so + 1], (unsigned long long)d64);
     if (ev != NO_EVENT) atomicMin(a.event, ev);

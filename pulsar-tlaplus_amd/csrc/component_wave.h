@@ -71,6 +71,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
   const int mb = L.msg_sh + L.N * L.mw;
   if (lane < LV) lvl_sh[lane] = 0;
   u64 gen = 0, dist = 0;
+  u64 wexp = 0;  // the walks' code-state expansions (each once for all the walk's components)
   unsigned od0 = 0, od1 = 0, od2 = 0;
   unsigned long long ev = NO_EVENT;
   // (wave w walks batches w*M .. w*M+M-1; component (batch bm, lane) as in component_body.h)
@@ -344,6 +345,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
       const int nqw = (int)uni((uint32_t)wave_sum_u64((u64)nq));
       if (lane == 0 && nqw && tail > lvl_start) lvl_sh[level] += (unsigned long long)((tail - lvl_start) * nqw);
     }
+    wexp += (u64)head;  // (scalar: the walk's expanded code states)
     __syncthreads();  // (the next batches clear the table)
   }
   gen = wave_sum_u64(gen);
@@ -354,6 +356,7 @@ __device__ __forceinline__ void component_wave_body(const CompArgs& a, const Lay
   __syncthreads();
   const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy
   if (lane == 0) {
+    if (wexp && a.expansions) atomicAdd(&a.expansions[so], (unsigned long long)wexp);
     if (gen) atomicAdd(&a.totals[so + 0], (unsigned long long)gen);
     if (dist) atomicAdd(&a.totals[so + 1], (unsigned long long)dist);
     if (ev != NO_EVENT) atomicMin(a.event, ev);

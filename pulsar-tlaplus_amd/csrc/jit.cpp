@@ -101,9 +101,11 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
              "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ", " + od + ", " + code +
              ">(a, kL); }\n";
       }
-  // the per-lane code pass with a bitmap FPSet (component_lane.h)
+  // the per-lane code pass with a bitmap FPSet (component_lane.h; TLCG_LANE_ATTR:
+  // a tuning hook for its attributes, e.g. amdgpu_waves_per_eu)
+  s += "#ifndef TLCG_LANE_ATTR\n#define TLCG_LANE_ATTR\n#endif\n";
   for (const char* od : {"false", "true"})
-    s += std::string("extern \"C\" __global__ __launch_bounds__(64) void tlcg_componentp") +
+    s += std::string("extern \"C\" __global__ __launch_bounds__(64) TLCG_LANE_ATTR void tlcg_componentp") +
          (od[0] == 't' ? "od" : "") + "_64(tlcg::CompArgs a) { tlcg::component_lane_body<64, " + od + ">(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_384(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";

@@ -129,6 +129,7 @@ def load_library(path: str = LIB_PATH):
         "tlcg_copy_states_words": (C.c_int, [P, U64, U64, C.POINTER(U64)]),
         "tlcg_tlc_stop_stats": (C.c_int, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
         "tlcg_outdegree": (C.c_int, [P, C.POINTER(U64), I32, C.POINTER(I32)]),
+        "tlcg_expansions": (C.c_int, [P, C.POINTER(U64)]),
         "tlcg_absorb_records": (C.c_int, [P, P, U64, S]),
         "tlcg_stream": (P, [P]),
         "tlcg_peer_access": (C.c_int, [I32]),
@@ -507,6 +508,14 @@ class Checker:
         g, d, q = C.c_uint64(), C.c_uint64(), C.c_uint64()
         self._chk(self.lib.tlcg_tlc_stop_stats(self.ctx, C.byref(g), C.byref(d), C.byref(q)), "tlcg_tlc_stop_stats")
         return g.value, d.value, q.value
+
+    def expansions(self) -> int:
+        """state expansions the last check's kernels made (tlcg_expansions):
+        distinct / expansions is 1 for a per-state kernel, the components per
+        walk for the one-walk-per-wavefront kernel"""
+        n = C.c_uint64()
+        self._chk(self.lib.tlcg_expansions(self.ctx, C.byref(n)), "tlcg_expansions")
+        return n.value
 
     def outdegree(self) -> List[int]:
         """TLC's outdegree histogram of the completed check (tlcg_outdegree):

@@ -5,7 +5,8 @@
 CASE = name:cfg[:rank/world][|ENV=V,ENV2=V][|DEF=1;DEF2]
   cfg: s, m8, g9, g9deep, p8 (bench.py's CONFIGS)
   rank/world: a closed partition's share (e.g. 0/8: the first of 8 ranks)
-  ENV: environment for the run (TLCG_COMP_GRID=3072, TLCG_TREE_G=2, ...;
+  ENV: environment for the run (TLCG_COMP_GRID=3072, TLCG_TREE_G=2, ...; several
+       joined by ',' or '+';
        PROBE_ENGINE=global, PROBE_TLC=1: TLC order)
   DEF: hipRTC define set (TLCG_JIT_DEFINES, e.g. TLCG_LDS_COLS=0)
 Each case builds its own context, runs 3 complete checks, and reports the
@@ -32,7 +33,7 @@ for spec in sys.argv[1:]:
     defs = parts[2] if len(parts) > 2 else ""
     os.environ.clear()
     os.environ.update(base_env)
-    for kv in filter(None, envs.split(",")):
+    for kv in filter(None, envs.replace("+", ",").split(",")):  # ('+' too: gpu.sh splits cases on ',')
         k, v = kv.split("=", 1)
         os.environ[k] = v
     if defs:

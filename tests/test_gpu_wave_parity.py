@@ -219,3 +219,29 @@ def test_g9_wave_module_m_override(defines, monkeypatch):
         assert got == order
     finally:
         ck.close()
+
+
+@pytest.mark.parametrize("mode", ["perlane", "perlane_body", "wave", "global"])
+def test_expansions_count(mode, monkeypatch):
+    """tlcg_expansions, the kernels' own count of state expansions: a per-lane
+    kernel expands every distinct state once (distinct / expansions = 1), the
+    one-walk-per-wavefront kernel each code state of a walk once for all its
+    components (M8: ceil(11^6 / 64 / M) walks x 62 code states), the global
+    engine each stored level once"""
+    m = tlcgpu.Model(key_space=range(1, 11), value_space=range(1, 11))
+    if mode != "global":
+        set_mode(monkeypatch, mode)
+    ck = tlcgpu.Checker(m, engine="global" if mode == "global" else "auto",
+                        log2_fpset_slots=28 if mode == "global" else 0)
+    try:
+        r = ck.run(with_trace=False)
+        assert (r.distinct, r.generated) == (109_836_782, 147_039_563)
+        x = ck.expansions()
+        if mode == "wave":
+            assert r.jit_used & 8
+            walks = -(-(-(-11 ** 6 // 64)) // 10)  # (M = 10: M8 is under WAVE_BIG_COMPS)
+            assert x == walks * 62, (x, walks)
+        else:
+            assert x == r.distinct, (mode, x, r.distinct)
+    finally:
+        ck.close()
