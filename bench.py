@@ -528,9 +528,10 @@ def main():
         # the wave kernels (component_wave.h, tree_wave.h): one walk of the code
         # graph per wavefront applied to M x 64 components -- a product
         # quotient, reported apart (engines.wave_quotient), never the headline
-        wave_run = time_engine("auto")
-        if not (wave_run["jit"] & (8 | 16)):
-            wave_run = None
+        if not open_model:
+            wave_run = time_engine("auto")
+            if not (wave_run["jit"] & (8 | 16)):
+                wave_run = None
     distinct, generated = cfg["distinct"], cfg["generated"]
     # (a producer-modelled cfg has one initial state; its Terminating stutters
     # are not counted out of the probes, so its bytes/state is an upper bound)
