@@ -101,6 +101,12 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
              "(tlcg::CompArgs a) { tlcg::component_body<" + std::to_string(K) + ", " + od + ", " + code +
              ">(a, kL); }\n";
       }
+  // the global engine's fast level (expand_fast.h), 2 parents per thread, load-then-CAS / CAS-only
+  // (one-word layouts only, the kernel's domain)
+  if (L.bits <= 63)
+    for (int probe : {0, 1})
+      s += std::string("extern \"C\" __global__ __launch_bounds__(256) void tlcg_expand_fast_2") + (probe ? "c" : "") +
+           "(tlcg::ExpandArgs a) { tlcg::expand_fast_body<2, " + std::to_string(probe) + ">(a, kL); }\n";
   // the per-lane code pass with a bitmap FPSet (component_lane.h; TLCG_LANE_ATTR:
   // a tuning hook for its attributes, e.g. amdgpu_waves_per_eu)
   s += "#ifndef TLCG_LANE_ATTR\n#define TLCG_LANE_ATTR\n#endif\n";
@@ -322,6 +328,11 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
     out->wave[0] = out->wave[1] = out->treew = nullptr;
     out->wave_m = WAVE_M;
   }
+  if (L.bits <= 63 && (hipModuleGetFunction(&out->expand_fast[0], out->module, "tlcg_expand_fast_2") != hipSuccess ||
+                       hipModuleGetFunction(&out->expand_fast[1], out->module, "tlcg_expand_fast_2c") != hipSuccess)) {
+    *err = "hipModuleGetFunction tlcg_expand_fast_2";
+    return false;
+  }
   if (hipModuleGetFunction(&out->lane[0], out->module, "tlcg_componentp_64") != hipSuccess ||
       hipModuleGetFunction(&out->lane[1], out->module, "tlcg_componentpod_64") != hipSuccess) {
     *err = "hipModuleGetFunction tlcg_componentp_64";
@@ -374,6 +385,15 @@ bool jit_launch_component(const JitKernels& k, const CompArgs& a, int K, bool co
   CompArgs copy = a;
   void* args[] = {&copy};
   return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
+}
+
+bool jit_launch_expand_fast(const JitKernels& k, const ExpandArgs& a, unsigned grid, int probe, hipStream_t stream) {
+  hipFunction_t f = k.expand_fast[probe ? 1 : 0];
+  if (!f) return false;
+  if (!grid) return true;
+  ExpandArgs copy = a;
+  void* args[] = {&copy};
+  return hipModuleLaunchKernel(f, grid, 1, 1, BLOCK, 1, 1, 0, stream, args, nullptr) == hipSuccess;
 }
 
 bool jit_launch_tree_wave(const JitKernels& k, const TreeArgs& a, hipStream_t stream) {

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "component.h"
+#include "expand_fast.h"
 #include "kernels.h"
 #include "tree.h"
 
@@ -28,6 +29,7 @@ struct JitKernels {
   hipFunction_t wave[2] = {nullptr, nullptr};     // codes, K = 64, one walk per wave (component_wave.h); outdegrees
   hipFunction_t treew = nullptr;                  // the tree's closed mode at 640 states, one walk per wave (tree_wave.h)
   hipFunction_t lane[2] = {nullptr, nullptr};     // codes, K = 64, per lane with a bitmap FPSet (component_lane.h); outdegrees
+  hipFunction_t expand_fast[2] = {nullptr, nullptr};  // the global engine's fast level (expand_fast.h), 2 parents per thread; PROBE 0 / 1
   int wave_m = WAVE_M;                            // its components per lane (the grid)
   std::string wave_error;                         // why the wave kernels are unset (jit_build), else empty
   hipFunction_t tree[4] = {nullptr, nullptr, nullptr, nullptr};  // component tree: 384 x 4 groups, 1024 x 1;
@@ -72,5 +74,7 @@ bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStr
 // lane-interleaved store, tree_wave_slot)
 bool jit_launch_tree_wave(const JitKernels& k, const TreeArgs& a, hipStream_t stream);
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream);
+// the global engine's fast level, layout-specialized (expand_fast.h): false when not built or on a launch error
+bool jit_launch_expand_fast(const JitKernels& k, const ExpandArgs& a, unsigned grid, int probe, hipStream_t stream);
 
 }  // namespace tlcg

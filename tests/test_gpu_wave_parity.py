@@ -245,3 +245,17 @@ def test_expansions_count(mode, monkeypatch):
             assert x == r.distinct, (mode, x, r.distinct)
     finally:
         ck.close()
+
+
+@pytest.mark.parametrize("case", FULL_CASES)
+def test_golden_case_global_specialized(case, monkeypatch):
+    """the global engine's fast level built layout-specialized (expand_fast.h
+    through jit.cpp, tlcg_stats.jit_used bit 6), forced onto the golden cases
+    with TLCG_JIT=1: the golden result (one-word layouts without a Producer
+    take the fast level; the others keep their kernels)"""
+    monkeypatch.setenv("TLCG_JIT", "1")
+    m = model_of(GOLDEN[case]["constants"])
+    r = tlcgpu.run(m, engine="global")
+    check_against_golden(case, r, False)
+    if tlcgpu.state_words(m) == 1 and not m.model_producer:
+        assert r.jit_used & 64, r.jit_used
