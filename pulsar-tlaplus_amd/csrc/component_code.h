@@ -47,6 +47,12 @@ namespace tlcg {
 
 typedef uint32_t ckey;  // component code
 
+// component_lane.h's per-lane FPSet: LANE_T slots (bits), the slot of code c
+// (c < 2^16) under a 24-bit multiplier: bits 24..31 of the low word of
+// c x mult (both operands 24-bit: one full-rate v_mul_u32_u24)
+constexpr int LANE_T = 256;
+TLCG_HD unsigned lane_slot(uint32_t c, uint32_t mult) { return ((c & 0xFFFFFFu) * (mult & 0xFFFFFFu)) >> 24; }
+
 // field offsets of a code (functions of the layout: constant-fold under hipRTC)
 TLCG_HD int cc_r(const Layout& L) { return L.C; }
 TLCG_HD int cc_h(const Layout& L) { return L.C + 1; }

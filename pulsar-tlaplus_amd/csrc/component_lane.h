@@ -178,7 +178,11 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
       if constexpr (OD) ocnt += alive ? 1u << (10 * (tail - tail0)) : 0u;  // new states this expansion discovered
       // the inserted successors' invariants (first failing + 1; INV_UNKNOWN
       // + 1: an outcome table left it to the programs, the rare branch)
-#ifndef TLCG_NO_INV  // (experiment only: measures what the invariants cost)
+#if defined(TLCG_LANE_INV_UNCOND) && !defined(TLCG_NO_INV)  // (A/B: both evaluated, no branch)
+      const int q1 = check_invariants_cbt(L, ccon, t) + 1, q2 = check_invariants_cbt(L, ccon, t2) + 1;
+      int ev1 = new1 ? q1 : 0;
+      int ev2 = new2 ? q2 : 0;
+#elif !defined(TLCG_NO_INV)  // (TLCG_NO_INV: experiment only, measures what the invariants cost)
       int ev1 = new1 ? check_invariants_cbt(L, ccon, t) + 1 : 0;
       int ev2 = new2 ? check_invariants_cbt(L, ccon, t2) + 1 : 0;
 #else

@@ -2,7 +2,6 @@
 // model-level (context-free) C-ABI entry points.
 #include "host_model.h"
 
-#include "component.h"
 #include "component_code.h"
 #include "component_model.h"
 
