@@ -86,14 +86,24 @@ def test_user_invariant_global_check_kernel(case, jit, monkeypatch):
         assert ck.tlc_stop_stats() == (want["generated"], want["distinct"], want["left_on_queue"])
 
 
+# the on-chip engines' first-pass kernels (tests/test_gpu_wave_parity.py): the
+# default (one walk per wavefront), the per-lane bitmap pass (component_lane.h)
+# and the per-lane pass of component_body.h
+KERNELS = {"default": {}, "perlane": {"TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "0"},
+           "perlane_body": {"TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "0", "TLCG_COMP_LANE": "0"}}
+
+
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
 @pytest.mark.parametrize("case", sorted(GOLD))
-def test_user_invariant_on_chip(case):
+def test_user_invariant_on_chip(case, kernel, monkeypatch):
     """the default engine with the user invariants inside its specialized
     kernels: the component engine without a Producer (its lanes keep TLC's
     order), the component tree's closed mode past a lane's 255 states (its
     error replayed in TLC's order on the host), the component tree with a
     Producer (its error reported by the global engine in TLC order); every
     error's trace and TLC's stop counters are TLC's, with no second run"""
+    for k, v in KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
     m = model(case)
     want = GOLD[case]["result"]
     # (C = 5: the local key passes 32 bits, or 302 states per component at K = 2: the tree's closed mode)
@@ -121,13 +131,16 @@ def test_user_invariant_on_chip(case):
 @pytest.mark.parametrize("utab", ["0", "dyn", "slow"])
 @pytest.mark.parametrize("case", ["U_LedgerCount", "U_all_hold", "U_ContextLedgerError", "U_mixed_user_first",
                                   "U_noretain_LatestIsLast", "U_C5_ContextBound"])
-def test_user_invariant_outcome_tables(case, utab, monkeypatch):
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
+def test_user_invariant_outcome_tables(case, utab, kernel, monkeypatch):
     """the outcome tables (component_code.h code_consts_user) against the
     programs: no tables (TLCG_UTAB=0), tables filled per component only
     (dyn), and every entry left to the kernel's fallback evaluation (slow)
     give the same verdict, counts, trace and stop counters as the default
     (host-made class tables + per-component ones) -- the golden fixture"""
     monkeypatch.setenv("TLCG_UTAB", utab)
+    for k, v in KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
     m = model(case)
     want = GOLD[case]["result"]
     ck = tlcgpu.Checker(m)
