@@ -150,6 +150,11 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
       const uint32_t o1 = owner[p1], o2 = owner[p2];
       const uint32_t w1 = bits[p1 >> 5][lane];
       uint32_t w2 = bits[p2 >> 5][lane];
+#ifndef TLCG_LANE_NO_SCHED_BARRIER
+      // (the four reads issued together, before anything that consumes them
+      // or writes LDS: one round trip per expansion, not two)
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       const uint32_t b1 = 1u << (p1 & 31), b2 = 1u << (p2 & 31);
       const bool e1 = alive && r == 1, e2 = alive && crash;
       const bool in1 = o1 == t + 1u, in2 = o2 == t2 + 1u;

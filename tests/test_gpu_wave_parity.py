@@ -93,7 +93,7 @@ def test_tlc_stop_statistics_kernel(case, mode, monkeypatch):
         ck.close()
 
 
-@pytest.mark.parametrize("mode", ["perlane", "perlane_body", "refuse_odd", "wave_big"])
+@pytest.mark.parametrize("mode", ["perlane", "refuse_odd"])
 @pytest.mark.parametrize("seed", range(40))
 def test_random_cfg_kernel(seed, mode, monkeypatch):
     """tests/test_gpu_random_cfgs.py's seeded constants on the default engine
