@@ -176,7 +176,9 @@ typedef struct tlcg_stats {
                                 hash injective on the component code set (tlcg_componentp_64,
                                 component_lane.h);
                                 bit 6: the global engine's fast level ran layout-specialized
-                                (tlcg_expand_fast_2, expand_fast.h) */
+                                (tlcg_expand_fast_2, expand_fast.h);
+                                bit 7: the component tree's closed pass ran with a bitmap FPSet
+                                over the host's perfect hash (tlcg_treecb_640, tree_body.h) */
   uint64_t host_states;      /* committed states spilled to host memory (tlcg_opts.spill) */
   uint64_t fpset_host_states; /* states held by the host FPSet tier (tlcg_opts.fpset_spill) */
   uint64_t transport;        /* multi-rank runs: 1 host threads + device copies, 2 RCCL; 0 one context */

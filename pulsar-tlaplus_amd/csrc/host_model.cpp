@@ -310,6 +310,26 @@ bool build_slot_disp(const HostModel& hm, int T, uint32_t mult, uint32_t* dmult,
   return false;
 }
 
+bool build_slot_owner(const HostModel& hm, int T, uint32_t mult, uint32_t dmult, const uint16_t* disp,
+                      uint32_t* owner) {
+  std::fill(owner, owner + T, 0u);
+  if (hm.L.producer || T <= 0) return false;
+  std::vector<std::vector<uint32_t>> calls;
+  std::vector<uint32_t> codes;
+  if (!comp0_calls(hm, T, 16, &calls, &codes)) return false;
+  for (uint32_t k : codes) {
+    unsigned sl = (unsigned)(((unsigned long long)(k * mult) * (unsigned)T) >> 32);  // (tree_body.h's slot)
+    sl += disp[(k * dmult) >> 24];
+    sl = sl >= (unsigned)T ? sl - (unsigned)T : sl;
+    if (owner[sl]) {
+      std::fill(owner, owner + T, 0u);
+      return false;
+    }
+    owner[sl] = k + 1u;
+  }
+  return true;
+}
+
 bool build_lane_phash(const HostModel& hm, uint32_t* mult, uint32_t* owner) {
   std::fill(owner, owner + LANE_T, 0u);
   *mult = 0;

@@ -60,6 +60,12 @@ uint32_t tune_slot_mult(const HostModel& hm, int T, int group, int candidates);
 // exact for any table (all zero: the plain multiply-shift slot).  False when
 // no table was found (then `disp` is all zero).
 bool build_slot_disp(const HostModel& hm, int T, uint32_t mult, uint32_t* dmult, uint16_t* disp);
+// the tree's closed mode with the bitmap FPSet (tree_body.h BITS): owner[s] =
+// the code of component 0's code set in slot s + 1 (0: none), T entries, under
+// the slot of build_slot_disp's (mult, dmult, disp); false unless every code
+// of the set has a slot of its own (then the bitmap pass is not used)
+bool build_slot_owner(const HostModel& hm, int T, uint32_t mult, uint32_t dmult, const uint16_t* disp,
+                      uint32_t* owner);
 
 // the per-lane bitmap pass (component_lane.h): a 24-bit multiplier under
 // which lane_slot (the top 8 bits of code x mult) is injective on component

@@ -123,6 +123,9 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
   s += "#ifndef TLCG_TREEC_G\n#define TLCG_TREEC_G 4\n#endif\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treec_640(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<640, 1024, TLCG_TREEC_G, true, " + w + ">(a, kL); }\n";
+  // (the same with the bitmap FPSet over the host's perfect hash, tree_body.h BITS)
+  s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treecb_640(tlcg::TreeArgs a) "
+       "{ tlcg::tree_body<640, 1024, TLCG_TREEC_G, true, " + w + ", true>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treec_2048(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<2048, 4096, 1, true, " + w + ">(a, kL); }\n";
   return s;
@@ -328,6 +331,10 @@ bool jit_build(const Layout& L, int device, JitKernels* out, std::string* err, c
     out->wave[0] = out->wave[1] = out->treew = nullptr;
     out->wave_m = WAVE_M;
   }
+  if (hipModuleGetFunction(&out->treeb, out->module, "tlcg_treecb_640") != hipSuccess) {
+    *err = "hipModuleGetFunction tlcg_treecb_640";
+    return false;
+  }
   if (L.bits <= 63 && (hipModuleGetFunction(&out->expand_fast[0], out->module, "tlcg_expand_fast_2") != hipSuccess ||
                        hipModuleGetFunction(&out->expand_fast[1], out->module, "tlcg_expand_fast_2c") != hipSuccess)) {
     *err = "hipModuleGetFunction tlcg_expand_fast_2";
@@ -404,6 +411,14 @@ bool jit_launch_tree_wave(const JitKernels& k, const TreeArgs& a, hipStream_t st
   // one wave per TLCG_TREE_WAVE_M batches of 64 components (the kernel strides over the rest)
   return hipModuleLaunchKernel(k.treew, tree_grid((a.n_comp + 63) / 64, TREE_WAVE_M), 1, 1, 64, 1, 1, 0, stream, args,
                                nullptr) == hipSuccess;
+}
+
+bool jit_launch_tree_bits(const JitKernels& k, const TreeArgs& a, hipStream_t stream) {
+  if (!a.n_comp) return true;
+  if (!k.treeb || !a.owner) return false;
+  TreeArgs copy = a;
+  void* args[] = {&copy};
+  return hipModuleLaunchKernel(k.treeb, tree_grid(a.n_comp, 4), 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
 }
 
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream) {

@@ -28,6 +28,7 @@ struct JitKernels {
   hipFunction_t code_od[2] = {nullptr, nullptr};
   hipFunction_t wave[2] = {nullptr, nullptr};     // codes, K = 64, one walk per wave (component_wave.h); outdegrees
   hipFunction_t treew = nullptr;                  // the tree's closed mode at 640 states, one walk per wave (tree_wave.h)
+  hipFunction_t treeb = nullptr;                  // the tree's closed mode at 640 states with the bitmap FPSet (tree_body.h BITS)
   hipFunction_t lane[2] = {nullptr, nullptr};     // codes, K = 64, per lane with a bitmap FPSet (component_lane.h); outdegrees
   hipFunction_t expand_fast[2] = {nullptr, nullptr};  // the global engine's fast level (expand_fast.h), 2 parents per thread; PROBE 0 / 1
   int wave_m = WAVE_M;                            // its components per lane (the grid)
@@ -74,6 +75,8 @@ bool jit_launch_user_check(const JitUserCheck& k, const UserCheckArgs& a, hipStr
 // lane-interleaved store, tree_wave_slot)
 bool jit_launch_tree_wave(const JitKernels& k, const TreeArgs& a, hipStream_t stream);
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream);
+// the closed tree at 640 states with the bitmap FPSet (tree_body.h BITS; TreeArgs::owner set)
+bool jit_launch_tree_bits(const JitKernels& k, const TreeArgs& a, hipStream_t stream);
 // the global engine's fast level, layout-specialized (expand_fast.h): false when not built or on a launch error
 bool jit_launch_expand_fast(const JitKernels& k, const ExpandArgs& a, unsigned grid, int probe, hipStream_t stream);
 

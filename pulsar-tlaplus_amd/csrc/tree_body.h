@@ -83,8 +83,18 @@ namespace tlcg {
 #ifndef TLCG_TREE_TSCALE_CLOSED
 #define TLCG_TREE_TSCALE_CLOSED 100
 #endif
-template <int CAP, int T, int G, bool CLOSED = false, typename W = u64>
+// BITS (closed mode, round 6): the FPSet of a component is one bit per slot
+// of the host's perfect hash (mult + disp) instead of a code + 1 per slot, with
+// a workgroup-shared table own[slot] = the code of the shared code set in that
+// slot + 1 (TreeArgs::owner).  FPSet.put(key) is exact for any key: key is
+// present iff own[slot(key)] = key + 1 and its bit is set (an LDS atomicOr
+// returns the old bit, so two lanes inserting one key agree on which is
+// first); a key outside the set raises TREE_OVERFLOW, and the 2048-state pass
+// (code + 1 tables, linear probing) takes the model.  A component's table is
+// CAP / 8 bytes instead of CAP x 4, so a CU holds more wavefronts.
+template <int CAP, int T, int G, bool CLOSED = false, typename W = u64, bool BITS = false>
 __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
+  static_assert(!BITS || CLOSED, "the bitmap FPSet needs the shared code set (closed mode)");
   constexpr int S = 64 / G;  // lanes per group
   static_assert((T & (T - 1)) == 0 && T >= CAP, "T: a power of 2 >= CAP");
   // FPSet slots per component.  Closed mode: TLCG_TREE_TSCALE_CLOSED % of
@@ -101,7 +111,9 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
 #endif
   static_assert(TT >= CAP, "an FPSet holds a whole component");
   constexpr bool TPOW2 = (TT & (TT - 1)) == 0;
-  __shared__ uint32_t h[G][TT];      // key + 1, 0 = empty
+  constexpr int HW = BITS ? (TT + 127) / 128 * 4 : TT;  // words per component's table (BITS: whole uint4s)
+  __shared__ uint32_t h[G][HW];      // key + 1, 0 = empty (BITS: one bit per slot)
+  __shared__ uint32_t own[BITS ? TT : 1];  // BITS: the code in each slot + 1
 #ifndef TLCG_TREE_KEYS_LDS
   // A depth's states are read back from the group's HBM chunk (written
   // before the __syncthreads that ends the insert step, so visible to the
@@ -148,6 +160,9 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   if constexpr (ND > 1) {
     for (int i = lane; i < ND; i += 64) dsp[i] = a.disp[i];
   }
+  if constexpr (BITS) {
+    for (int i = lane; i < TT; i += 64) own[i] = a.owner[i];
+  }
   __syncthreads();
   unsigned flags = 0;
   uint32_t maxn = 0;
@@ -184,7 +199,15 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         s = s >= (unsigned)TT ? s - (unsigned)TT : s;
       }
       int p0 = 0;
-      if constexpr (CLOSED ? TLCG_TREE_CAS1 : TLCG_TREE_CAS1_OPEN) {
+      if constexpr (BITS) {
+        if (own[s] == key + 1u) {
+          const uint32_t bit = 1u << (s & 31);
+          isnew = !(atomicOr(&hh[s >> 5], bit) & bit);
+        } else {
+          flags |= TREE_OVERFLOW;  // not the shared code set: the 2048-state pass takes the model
+        }
+        p0 = TT;  // (no probe loop)
+      } else if constexpr (CLOSED ? TLCG_TREE_CAS1 : TLCG_TREE_CAS1_OPEN) {
         // the first CAS outside the probe loop: with the perfect hash it
         // settles every insert, so the loop is skipped (no lane collides);
         // in Producer mode it settles most
@@ -252,7 +275,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   while (true) {
     // a group without a component takes its next one
     if (!have && ci < a.n_comp) {
-      for (int i = sub * 4; i < TT; i += S * 4) *reinterpret_cast<uint4*>(&hh[i]) = make_uint4(0, 0, 0, 0);
+      for (int i = sub * 4; i < HW; i += S * 4) *reinterpret_cast<uint4*>(&hh[i]) = make_uint4(0, 0, 0, 0);
       if constexpr (CLOSED) {
         np = 1;  // the component's initial state
         const W s0 = init_state<W>(L, a.comp0 + ci);

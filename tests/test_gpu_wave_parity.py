@@ -13,7 +13,8 @@ kernel is forced on them:
               bench.py's per-state headline -- tlcg_componentp_64 (component_lane.h,
               a bitmap FPSet) where its slot hash exists, else tlcg_componentc_64
               (component_body.h) / tlcg_treec_640
-  perlane_body  the same with TLCG_COMP_LANE=0: tlcg_componentc_64 throughout
+  perlane_body  the same with TLCG_COMP_LANE=0 and TLCG_TREE_BITS=0: tlcg_componentc_64
+              and the closed tree's code tables (tlcg_treec_640) throughout
   refuse_odd  TLCG_JIT=1 and the test hook TLCG_WAVE_REFUSE_ODD: the components
               of odd batch + lane parity refuse the walk, so the walk-join
               fallback (component_wave.h) and the 32-bit cascade pass run
@@ -35,7 +36,8 @@ MODES = {
     "wave": {"TLCG_JIT": "1"},
     "wave_big": {"TLCG_JIT": "1", "TLCG_WAVE_BIG_COMPS": "1"},
     "perlane": {"TLCG_JIT": "1", "TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "0"},
-    "perlane_body": {"TLCG_JIT": "1", "TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "0", "TLCG_COMP_LANE": "0"},
+    "perlane_body": {"TLCG_JIT": "1", "TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "0", "TLCG_COMP_LANE": "0",
+                     "TLCG_TREE_BITS": "0"},
     "refuse_odd": {"TLCG_JIT": "1", "TLCG_JIT_DEFINES": "TLCG_WAVE_REFUSE_ODD=1"},
 }
 
@@ -54,6 +56,8 @@ def check_kernel(mode, r):
             assert not r.jit_used & 32, r.jit_used
     if r.engine == "tree" and mode.startswith("perlane"):
         assert not r.jit_used & 16, r.jit_used
+        if mode == "perlane_body":
+            assert not r.jit_used & 128, r.jit_used
 
 
 @pytest.mark.parametrize("mode", sorted(MODES))
@@ -259,3 +263,15 @@ def test_golden_case_global_specialized(case, monkeypatch):
     check_against_golden(case, r, False)
     if tlcgpu.state_words(m) == 1 and not m.model_producer:
         assert r.jit_used & 64, r.jit_used
+
+
+@pytest.mark.parametrize("case", ["W_C12", "W_C12_k1", "W_C12_noretain", "W_C12_leak", "W_C12_dup"])
+def test_tree_bits_pass_runs(case, monkeypatch):
+    """the closed tree's per-state pass with the bitmap FPSet (tree_body.h
+    BITS, jit_used bit 7) takes the wide golden cases when its perfect hash
+    exists: the golden result"""
+    set_mode(monkeypatch, "perlane")
+    m = model_of(GOLDEN[case]["constants"])
+    r = tlcgpu.run(m)
+    check_against_golden(case, r, False)
+    assert r.engine == "tree" and r.jit_used & 128 and not r.jit_used & 16, r.jit_used
