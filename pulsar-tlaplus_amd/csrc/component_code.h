@@ -389,6 +389,60 @@ TLCG_HD int compactor_step_cb(const Layout& L, const CodeConsts& K, ckey c, ckey
   return res;
 }
 
+// compactor_step_cb as update masks (round 6, the per-lane kernel
+// component_lane.h): the disjunct's successor of code c depends on c only
+// through its phase, whether readPosition is set (r) and its largest present
+// ledger m (:103-106) -- the bits it sets and clears -- and, for
+// PersistCusror, two fields it copies (cursor horizon := horizon, cursor
+// context := context, :149).  So each (phase, r, m) has one entry: the bits
+// set, the bits cleared, the copied fields' mask and the result (0 disabled,
+// 1 enabled, 2 evaluation error), and a lane forms its state's successor as
+// (c & ~clear) | set | (copied & mask).  Index ph | r << 3 | m << 4: 64
+// entries for C <= 3 (the 16-bit codes of the per-lane kernel).  Checked
+// against compactor_step_cb on every code (tlcg_host_component_selfcheck).
+constexpr int STEP_TAB = 64;
+TLCG_HD u64 compactor_step_entry(const Layout& L, int idx) {
+  const int ph = idx & 7, r = (idx >> 3) & 1, m = idx >> 4;
+  const uint32_t xm = lmask(L.ctx_w) << cc_x(L), ccm = lmask(L.curc_w) << cc_cc(L);
+  uint32_t set = 0, clr = 7u << cc_ph(L), cpy = 0;
+  int res = 0;
+  if (ph == PH_ONE) {  // :96-97, readPosition := Len (enabled while it is Nil and Len > 0)
+    set = 1u << cc_r(L);
+    res = r ? 0 : 1;
+  } else if (ph == PH_WRITE) {  // :124-130, ledger m + 1
+    set = m < L.C ? 1u << m : 0u;
+    res = r && m < L.C ? 1 : 0;
+  } else if (ph == PH_UCTX) {  // :137, context := m
+    clr |= xm;
+    set = ((uint32_t)m << cc_x(L)) & xm;
+    res = 1;
+  } else if (ph == PH_UHOR) {  // :143, horizon := readPosition
+    set = 1u << cc_h(L);
+    res = r ? 1 : 2;
+  } else if (ph == PH_PERSIST) {  // :149, cursor := [horizon, context]
+    set = 1u << cc_cp(L);
+    clr |= (1u << cc_ch(L)) | ccm;
+    cpy = (1u << cc_ch(L)) | ccm;
+    res = 1;
+  } else if (ph == PH_DELETE) {  // :156-163, readPosition := Nil, ledger m - 1 deleted
+    clr |= (1u << cc_r(L)) | (m >= 2 ? 1u << (m - 2) : 0u);
+    res = m == 0 ? 2 : 1;
+  }
+  set |= (ph >= PH_DELETE ? (uint32_t)PH_ONE : (uint32_t)ph + 1) << cc_ph(L);
+  return (u64)set | ((u64)clr << 16) | ((u64)cpy << 32) | ((u64)res << 48);
+}
+// compactor_step_cb through the entries (tab: STEP_TAB of them)
+TLCG_HD int compactor_step_tab(const Layout& L, const CodeConsts& K, const u64* tab, ckey c, ckey* t, int* act) {
+  const uint32_t ph = cget(c, cc_ph(L), 3), r = (c >> cc_r(L)) & 1;
+  const u64 e = tab[ph | (r << 3) | ((uint32_t)c_max_ledger(L, c) << 4)];
+  const uint32_t set = (uint32_t)e & 0xFFFFu, clr = (uint32_t)(e >> 16) & 0xFFFFu, cpy = (uint32_t)(e >> 32) & 0xFFFFu;
+  const uint32_t copied = (((c >> cc_h(L)) & 1u) << cc_ch(L)) | (cget(c, cc_x(L), L.ctx_w) << cc_cc(L));
+  *t = (c & ~clr) | set | (copied & cpy);
+  const int res = ph == PH_ONE && K.len == 0 ? 0 : (int)(e >> 48);
+  if (res) *act = ACT_PHASEONE + (int)ph;
+  return res;
+}
+
 // BrokerCrash, compaction.tla:169-182.  Returns 1 if enabled.
 TLCG_HD int crash_step_c(const Layout& L, ckey c, ckey* t) {
   const uint32_t cr = cget(c, cc_cr(L), L.cr_w);

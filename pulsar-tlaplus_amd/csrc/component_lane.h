@@ -45,6 +45,12 @@ namespace tlcg {
 #define TLCG_LANE_R 16
 #endif
 constexpr int LANE_R = TLCG_LANE_R;  // FIFO ring entries per lane (a power of 2)
+// the compactor disjunct through its update masks (component_code.h
+// compactor_step_tab: one LDS read and a few bit operations instead of the six
+// candidate successors of compactor_step_cb); 0: compactor_step_cb (A/B)
+#ifndef TLCG_LANE_STEP_TAB
+#define TLCG_LANE_STEP_TAB 1
+#endif
 
 // the sum over the wave of x (every lane active), in a scalar
 __device__ __forceinline__ uint32_t lane_wave_sum(uint32_t x) {
@@ -65,10 +71,16 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
   __shared__ uint32_t bits[NW][64];            // the lanes' FPSets: bit s of lane l = bit s % 32 of bits[s / 32][l]
   __shared__ uint32_t owner[T];                // the code in slot s + 1 (0: none), shared
   __shared__ unsigned long long lvl_sh[LV];    // per level: distinct (low 32) + generated (high 32)
+#if TLCG_LANE_STEP_TAB
+  __shared__ u64 steps[STEP_TAB];              // the compactor disjunct's update masks (compactor_step_entry)
+#endif
   const int lane = threadIdx.x;
   const int mb = L.msg_sh + L.N * L.mw;
   const uint32_t mult = a.lane_mult;
   for (int i = lane; i < T; i += 64) owner[i] = a.lane_owner[i];
+#if TLCG_LANE_STEP_TAB
+  for (int i = lane; i < STEP_TAB; i += 64) steps[i] = compactor_step_entry(L, i);
+#endif
   if (lane < LV) lvl_sh[lane] = 0;
   uint32_t gen = 0, dist = 0, nexp = 0;  // (nexp: states expanded by the components that finish here)
   unsigned od0 = 0, od1 = 0, od2 = 0;
@@ -143,7 +155,11 @@ __device__ __forceinline__ void component_lane_body(const CompArgs& a, const Lay
       const ckey nxt = ring[(head + 1) & (R - 1)][lane];
       ckey t = 0, t2 = 0;
       int action = 0;
-      const int r = compactor_step_cb(L, ccon, s, &t, &action);  // compaction.tla:221-226
+#if TLCG_LANE_STEP_TAB
+      const int r = compactor_step_tab(L, ccon, steps, s, &t, &action);  // compaction.tla:221-226
+#else
+      const int r = compactor_step_cb(L, ccon, s, &t, &action);
+#endif
       const bool crash = crash_step_c(L, s, &t2) != 0;            // :227
       // FPSet.put of both successors: slot, the shared owner, the lane's bits
       const unsigned p1 = lane_slot(t, mult), p2 = lane_slot(t2, mult);

@@ -796,13 +796,19 @@ int64_t tlcg_host_component_selfcheck(const tlcg_model* m, uint64_t first, uint6
       // the kernel's branch-free code functions vs the branching ones on every
       // code of the first components, reachable or not
       const CodeConsts kc = code_consts(L, cm);
+      u64 tab[STEP_TAB];
+      for (int i = 0; i < STEP_TAB; ++i) tab[i] = compactor_step_entry(L, i);
       for (ckey cd = 0; cd < (1u << code_bits(L)); ++cd) {
-        ckey t1 = 0, t2 = 0;
-        int a1 = -1, a2 = -1;
+        ckey t1 = 0, t2 = 0, t3 = 0;
+        int a1 = -1, a2 = -1, a3 = -1;
         const int r1 = compactor_step_c(L, kc, cd, c_phase(L, cd), &t1, &a1);
         const int r2 = compactor_step_cb(L, kc, cd, &t2, &a2);
         if (r1 != r2 || a1 != a2 || (r1 == 1 && t1 != t2) || check_invariants_c(L, kc, cd) != check_invariants_cb(L, kc, cd))
           return -(1 + checked);
+        if (L.C <= 3) {  // the per-lane kernel's table form (component_lane.h)
+          const int r3 = compactor_step_tab(L, kc, tab, cd, &t3, &a3);
+          if (r3 != r1 || a3 != a1 || (r1 == 1 && t3 != t1)) return -(1 + checked);
+        }
       }
     }
     std::unordered_set<u64> seen{s0};
