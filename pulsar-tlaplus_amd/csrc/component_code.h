@@ -51,7 +51,17 @@ typedef uint32_t ckey;  // component code
 // (c < 2^16) under a 24-bit multiplier: bits 24..31 of the low word of
 // c x mult (both operands 24-bit: one full-rate v_mul_u32_u24)
 constexpr int LANE_T = 256;
-TLCG_HD unsigned lane_slot(uint32_t c, uint32_t mult) { return ((c & 0xFFFFFFu) * (mult & 0xFFFFFFu)) >> 24; }
+TLCG_HD unsigned lane_slot(uint32_t c, uint32_t mult) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // (one full-rate v_mul_u32_u24: from the C form the compiler picks the
+  // quarter-rate v_mul_lo_u32, __umul24 included)
+  uint32_t p;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(p) : "v"(c), "v"(mult));
+  return p >> 24;
+#else
+  return ((c & 0xFFFFFFu) * (mult & 0xFFFFFFu)) >> 24;
+#endif
+}
 
 // field offsets of a code (functions of the layout: constant-fold under hipRTC)
 TLCG_HD int cc_r(const Layout& L) { return L.C; }
