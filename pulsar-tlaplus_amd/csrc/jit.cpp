@@ -31,7 +31,11 @@ std::string layout_literal(const Layout& L) {
 #undef F
   o << ".inv = {";
   for (int i = 0; i < 8; ++i) o << L.inv[i] << (i < 7 ? ", " : "");
-  o << "}, .msgs_mask = " << L.msgs_mask << "ull, .led_present_mask = " << L.led_present_mask << "ull};\n";
+  // (every field: defer_inv keeps the specialized global-engine expand from
+  // evaluating user invariants, which its level's check kernel evaluates)
+  o << "}, .defer_inv = " << L.defer_inv << ", .msgs_mask = " << L.msgs_mask << "ull, .led_present_mask = "
+    << L.led_present_mask << "ull, .msgs_mask_hi = " << L.msgs_mask_hi << "ull, .led_present_mask_hi = "
+    << L.led_present_mask_hi << "ull};\n";
   return o.str();
 }
 

@@ -93,6 +93,31 @@ KERNELS = {"default": {}, "perlane": {"TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "
            "perlane_body": {"TLCG_COMP_WAVE": "0", "TLCG_TREE_WAVE": "0", "TLCG_COMP_LANE": "0"}}
 
 
+@pytest.mark.parametrize("case", ["U_LedgerCount", "U_all_hold", "U_ContextLedgerError", "U_mixed_user_first",
+                                  "U_noretain_LatestIsLast"])
+def test_user_invariant_global_fast_specialized(case, monkeypatch):
+    """the global engine in fast order with the layout-specialized expand
+    (expand_fast.h, jit_used bit 6; TLCG_JIT=1 forces it on these small
+    models): the expand kernel leaves the user invariants to the level's
+    check kernel (Layout.defer_inv, which the specialized layout must carry),
+    so the verdict, depth and end-of-level counts are the fixture's"""
+    monkeypatch.setenv("TLCG_JIT", "1")
+    m = model(case)
+    want = GOLD[case]["result"]
+    ck = tlcgpu.Checker(m, engine="global")
+    try:
+        r = ck.run()
+        assert r.jit_used & 64 and r.jit_used & 4, r.jit_used
+        assert r.status == want["result"] and r.depth == want["depth"], (case, r.status, r.depth)
+        if want["result"] == "ok":
+            assert (r.generated, r.distinct) == (want["generated"], want["distinct"])
+        else:
+            assert (r.generated, r.distinct) == (want["eol_generated"], want["eol_distinct"])
+            assert r.invariant == want.get("invariant", r.invariant)
+    finally:
+        ck.close()
+
+
 @pytest.mark.parametrize("kernel", sorted(KERNELS))
 @pytest.mark.parametrize("case", sorted(GOLD))
 def test_user_invariant_on_chip(case, kernel, monkeypatch):
