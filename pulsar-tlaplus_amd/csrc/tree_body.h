@@ -130,23 +130,32 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   // store only past them -- no HBM load (behind the previous depth's stores)
   // and no re-encode on the common path.  0 = off.  Closed mode: 16 (G9-deep
   // 35.2 -> 31.2 ms with 640-slot tables, profiles/r02_tree_fb_ab.jsonl; a
-  // depth of G9-deep holds 7.5 states on average); Producer mode: off (P8
-  // 2.06 vs 2.09 / 2.20 ms at 32 / 16).
+  // depth of G9-deep holds 7.5 states on average); Producer mode: 48, in the
+  // LDS the 32-bit depth counts for 64 depths leave below the 10 KB that
+  // keeps 16 workgroups per CU (P8 1.82-1.85 -> 1.58-1.59 ms; 16 / 24 / 32 /
+  // 40: 1.71 / 1.67 / 1.61-1.62 / 1.59, profiles/r06_probe_p8_fb.jsonl; in
+  // round 2, with 64-bit counts for 128 depths, any buffer crossed 10 KB and
+  // measured slower)
 #ifndef TLCG_TREE_FB
 #define TLCG_TREE_FB 16
 #endif
 #ifndef TLCG_TREE_FB_OPEN
-#define TLCG_TREE_FB_OPEN 0
+#define TLCG_TREE_FB_OPEN 48
 #endif
   constexpr int FB = KCAP == CAP ? 0 : CLOSED ? TLCG_TREE_FB : TLCG_TREE_FB_OPEN;
   __shared__ uint32_t fbuf[G][2][FB > 0 ? FB : 1];
   int dbase = 0;  // the first position of the depth being inserted (FB)
-#ifdef TLCG_TREE_LVL32
-  typedef unsigned int lvl_t;  // a workgroup's per-depth sums fit 32 bits (it runs far fewer than 2^32 / CAP states)
-#else
-  typedef unsigned long long lvl_t;
+  // per-depth counts: 32 bits (a workgroup runs far fewer than 2^32 states
+  // at one depth); LDS sums for the first LV depths, global atomics on the
+  // workgroup's striped copy past them (Producer mode: deep components are
+  // rare and the LDS goes to the frontier buffer)
+  typedef unsigned int lvl_t;
+#ifndef TLCG_TREE_LVL_DEPTHS_OPEN
+#define TLCG_TREE_LVL_DEPTHS_OPEN 64
 #endif
-  __shared__ lvl_t lvl_d[TREE_MAXLV], lvl_g[TREE_MAXLV];
+  constexpr int LV = CLOSED ? TREE_MAXLV : TLCG_TREE_LVL_DEPTHS_OPEN;
+  static_assert(LV <= TREE_MAXLV, "the host sums TREE_MAXLV depths");
+  __shared__ lvl_t lvl_d[LV], lvl_g[LV];
   constexpr int ND = CLOSED && TLCG_TREE_DISP ? TREE_DISP : 1;
   __shared__ uint16_t dsp[ND];
   const int lane = threadIdx.x;
@@ -156,7 +165,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   const int mb = L.msg_sh + L.N * L.mw;  // `messages` (with its length) occupies the low mb bits
   int log2t = 0;
   while ((1 << log2t) < TT) ++log2t;
-  for (int i = lane; i < TREE_MAXLV; i += 64) lvl_d[i] = lvl_g[i] = 0;
+  for (int i = lane; i < LV; i += 64) lvl_d[i] = lvl_g[i] = 0;
   if constexpr (ND > 1) {
     for (int i = lane; i < ND; i += 64) dsp[i] = a.disp[i];
   }
@@ -435,8 +444,14 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       for (int off = S / 2; off > 0; off >>= 1) gen += __shfl_xor(gen, off);
     }
     if (have && sub == S - 1 && d < TREE_MAXLV && a.count) {
-      atomicAdd(&lvl_d[d], (lvl_t)(f1 - f0));
-      atomicAdd(&lvl_g[d], (lvl_t)gen);
+      if (d < LV) {
+        atomicAdd(&lvl_d[d], (lvl_t)(f1 - f0));
+        atomicAdd(&lvl_g[d], (lvl_t)gen);
+      } else {
+        const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;
+        atomicAdd(&a.lvl[so + d], (unsigned long long)(f1 - f0));
+        atomicAdd(&a.lvl_gen[so + d], (unsigned long long)gen);
+      }
     }
     __syncthreads();
     if (have) {
@@ -458,7 +473,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   }
   __syncthreads();
   const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy
-  for (int i = lane; i < TREE_MAXLV; i += 64) {
+  for (int i = lane; i < LV; i += 64) {
     if (lvl_d[i]) atomicAdd(&a.lvl[so + i], (unsigned long long)lvl_d[i]);
     if (lvl_g[i]) atomicAdd(&a.lvl_gen[so + i], (unsigned long long)lvl_g[i]);
   }

@@ -49,6 +49,30 @@ def test_tree_matches_golden(case):
         ck.close()
 
 
+@pytest.mark.parametrize("case", OK_CASES)
+def test_tree_depth_counts_past_the_lds_sums(case, monkeypatch):
+    """Producer mode sums the first TLCG_TREE_LVL_DEPTHS_OPEN depths' counts in
+    LDS and adds deeper ones straight to the striped global counters
+    (tree_body.h); with 4 LDS depths every deeper depth takes that path and the
+    levels and generated counts stay the golden ones"""
+    monkeypatch.setenv("TLCG_JIT", "1")
+    monkeypatch.setenv("TLCG_JIT_DEFINES", "TLCG_TREE_LVL_DEPTHS_OPEN=4")
+    m = model_of(GOLDEN[case]["constants"])
+    if tlcgpu.state_words(m) != 1:
+        pytest.skip("a wide layout: the global engine")
+    want = GOLDEN[case]["result"]
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run()
+        assert r.engine == "tree" and r.jit_used & 1
+        assert (r.status, r.generated, r.distinct, r.depth) == ("ok", want["generated"], want["distinct"], want["depth"])
+        assert r.levels == want["levels"]
+        g = ck.level_generated()
+        assert len(g) == r.depth + 1 and sum(g) == r.generated
+    finally:
+        ck.close()
+
+
 @pytest.mark.parametrize("case", ["P_published"])
 def test_tree_parent_log_walks_to_init(case):
     """Sampled stored states (positions < 60 of random components of layers
