@@ -208,6 +208,16 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         s = s >= (unsigned)TT ? s - (unsigned)TT : s;
       }
       int p0 = 0;
+      // the probe step.  Producer mode: an odd step from a second hash of the
+      // key (double hashing; TLCG_TREE_DH=0: 1, linear probing).  A wave's
+      // insert waits for its longest probe sequence, and linear probing's
+      // primary clusters at the tables' final load (~0.7) made that long:
+      // P8 1.62 -> 1.40 ms (profiles/r06_probe_p8_dh.jsonl).  Closed mode
+      // places every code at its first slot (the host's perfect hash)
+#ifndef TLCG_TREE_DH
+#define TLCG_TREE_DH 1
+#endif
+      const unsigned step = TLCG_TREE_DH && !CLOSED && TPOW2 ? ((key * 0x85EBCA6Bu) >> (32 - log2t)) | 1u : 1u;
       if constexpr (BITS) {
         if (own[s] == key + 1u) {
           const uint32_t bit = 1u << (s & 31);
@@ -223,7 +233,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
         const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
         isnew = old == 0;
         p0 = old == 0 || old == key + 1u ? TT : 1;
-        s = s + 1 == (unsigned)TT ? 0u : s + 1;
+        s = TPOW2 ? (s + step) & (TT - 1) : (s + 1 == (unsigned)TT ? 0u : s + 1);
       }
       for (int p = p0; p < TT; ++p) {
         const uint32_t old = atomicCAS(&hh[s], 0u, key + 1u);
@@ -240,7 +250,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
           }
           if (old == key + 1u) break;
         }
-        s = TPOW2 ? (s + 1) & (TT - 1) : (s + 1 == (unsigned)TT ? 0u : s + 1);
+        s = TPOW2 ? (s + step) & (TT - 1) : (s + 1 == (unsigned)TT ? 0u : s + 1);
       }
     }
     const u64 m = __ballot(isnew) & gmask;

@@ -2,7 +2,10 @@
 specialized for a cfg (TLCG_JIT_DUMP) and compile it offline with hipcc to
 gfx950 assembly, so the ISA of the specialized kernels can be read.
 
-    python scripts/jit_isa.py [keys] [out_prefix]   -> out_prefix.hip, out_prefix.s
+    python scripts/jit_isa.py [keys|cfg] [out_prefix]   -> out_prefix.hip, out_prefix.s
+
+keys: KeySpace = ValueSpace = 1..keys (G9's constants otherwise); cfg: one
+of bench.py's CONFIGS (s, m8, g9, g9deep, p8).
 """
 import ctypes as C
 import os
@@ -13,11 +16,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pulsar-tlaplus_amd", "python"))
 import tlcgpu  # noqa: E402
 
-k = int(sys.argv[1]) if len(sys.argv) > 1 else 15
+arg = sys.argv[1] if len(sys.argv) > 1 else "15"
 out = sys.argv[2] if len(sys.argv) > 2 else "/tmp/g9jit"
 os.environ["TLCG_JIT_DUMP"] = out + ".hip"
 os.environ["TLCG_JIT_CACHE"] = "/tmp/tlcg-jit-isa-nocache"
-m = tlcgpu.Model(key_space=range(1, k + 1), value_space=range(1, k + 1))
+if arg.isdigit():
+    m = tlcgpu.Model(key_space=range(1, int(arg) + 1), value_space=range(1, int(arg) + 1))
+else:
+    sys.path.insert(0, ROOT)
+    from bench import model_for  # noqa: E402
+    m = model_for(arg)
 cm = m.to_c()
 err = C.create_string_buffer(8192)
 n = tlcgpu.load_library().tlcg_jit_selftest(C.byref(cm), b"gfx950", err, 8192)
