@@ -128,8 +128,9 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treec_640(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<640, 1024, TLCG_TREEC_G, true, " + w + ">(a, kL); }\n";
   // (the same with the bitmap FPSet over the host's perfect hash, tree_body.h BITS)
+  s += "#ifndef TLCG_TREECB_G\n#define TLCG_TREECB_G " + std::to_string(TREECB_G) + "\n#endif\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treecb_640(tlcg::TreeArgs a) "
-       "{ tlcg::tree_body<640, 1024, TLCG_TREEC_G, true, " + w + ", true>(a, kL); }\n";
+       "{ tlcg::tree_body<640, 1024, TLCG_TREECB_G, true, " + w + ", true>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treec_2048(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<2048, 4096, 1, true, " + w + ">(a, kL); }\n";
   return s;
@@ -422,7 +423,8 @@ bool jit_launch_tree_bits(const JitKernels& k, const TreeArgs& a, hipStream_t st
   if (!k.treeb || !a.owner) return false;
   TreeArgs copy = a;
   void* args[] = {&copy};
-  return hipModuleLaunchKernel(k.treeb, tree_grid(a.n_comp, 4), 1, 1, 64, 1, 1, 0, stream, args, nullptr) == hipSuccess;
+  return hipModuleLaunchKernel(k.treeb, tree_grid(a.n_comp, TREECB_G), 1, 1, 64, 1, 1, 0, stream, args, nullptr) ==
+         hipSuccess;
 }
 
 bool jit_launch_tree(const JitKernels& k, const TreeArgs& a, int cap, hipStream_t stream) {

@@ -265,12 +265,17 @@ def test_golden_case_global_specialized(case, monkeypatch):
         assert r.jit_used & 64, r.jit_used
 
 
+@pytest.mark.parametrize("groups", ["", "TLCG_TREECB_G=4"])
 @pytest.mark.parametrize("case", ["W_C12", "W_C12_k1", "W_C12_noretain", "W_C12_leak", "W_C12_dup"])
-def test_tree_bits_pass_runs(case, monkeypatch):
+def test_tree_bits_pass_runs(case, groups, monkeypatch):
     """the closed tree's per-state pass with the bitmap FPSet (tree_body.h
     BITS, jit_used bit 7) takes the wide golden cases when its perfect hash
-    exists: the golden result"""
+    exists: the golden result, at its 16 components per wavefront (tree.h
+    TREECB_G) and at 4 (the module's define; the host's grid stays sized for
+    16, and the kernel strides over the rest)"""
     set_mode(monkeypatch, "perlane")
+    if groups:
+        monkeypatch.setenv("TLCG_JIT_DEFINES", groups)
     m = model_of(GOLDEN[case]["constants"])
     r = tlcgpu.run(m)
     check_against_golden(case, r, False)
