@@ -142,7 +142,13 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
 #ifndef TLCG_TREE_FB_OPEN
 #define TLCG_TREE_FB_OPEN 48
 #endif
-  constexpr int FB = KCAP == CAP ? 0 : CLOSED ? TLCG_TREE_FB : TLCG_TREE_FB_OPEN;
+  // (closed mode's bitmap pass, 16 groups per wavefront: 48 keys; G9-deep
+  // 16 / 32 / 48 / 64: 9.0-9.6 / 7.9 / 7.3 / 8.4 ms on one box,
+  // profiles/r06_probe_treecb_g.jsonl)
+#ifndef TLCG_TREE_FB_BITS
+#define TLCG_TREE_FB_BITS 48
+#endif
+  constexpr int FB = KCAP == CAP ? 0 : CLOSED ? (BITS ? TLCG_TREE_FB_BITS : TLCG_TREE_FB) : TLCG_TREE_FB_OPEN;
   __shared__ uint32_t fbuf[G][2][FB > 0 ? FB : 1];
   int dbase = 0;  // the first position of the depth being inserted (FB)
   // per-depth counts: 32 bits (a workgroup runs far fewer than 2^32 states
