@@ -130,18 +130,17 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   // store only past them -- no HBM load (behind the previous depth's stores)
   // and no re-encode on the common path.  0 = off.  Closed mode: 16 (G9-deep
   // 35.2 -> 31.2 ms with 640-slot tables, profiles/r02_tree_fb_ab.jsonl; a
-  // depth of G9-deep holds 7.5 states on average); Producer mode: 40, in the
+  // depth of G9-deep holds 7.5 states on average); Producer mode: 48, in the
   // LDS the 32-bit depth counts for 64 depths leave below the 10 KB that
   // keeps 16 workgroups per CU (P8 1.82-1.85 -> 1.58-1.59 ms; 16 / 24 / 32 /
   // 40 / 48: 1.71 / 1.67 / 1.61-1.62 / 1.59 / 1.58-1.59,
-  // profiles/r06_probe_p8_fb.jsonl; 40 keys need no padding below, FBS = 80;
-  // in round 2, with 64-bit counts for 128 depths, any buffer crossed 10 KB
-  // and measured slower)
+  // profiles/r06_probe_p8_fb.jsonl; in round 2, with 64-bit counts for 128
+  // depths, any buffer crossed 10 KB and measured slower)
 #ifndef TLCG_TREE_FB
 #define TLCG_TREE_FB 16
 #endif
 #ifndef TLCG_TREE_FB_OPEN
-#define TLCG_TREE_FB_OPEN 40
+#define TLCG_TREE_FB_OPEN 48
 #endif
   // (closed mode's bitmap pass, 16 groups per wavefront: 48 keys; G9-deep
   // 16 / 32 / 48 / 64: 9.0-9.6 / 7.9 / 7.3 / 8.4 ms on one box,
@@ -150,16 +149,11 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
 #define TLCG_TREE_FB_BITS 48
 #endif
   constexpr int FB = KCAP == CAP ? 0 : CLOSED ? (BITS ? TLCG_TREE_FB_BITS : TLCG_TREE_FB) : TLCG_TREE_FB_OPEN;
-  // a group's two buffers, FBS words apart from the next group's: FBS = S
-  // (mod 32), so the S lanes of each group in a 32-lane half of the wave
-  // read (ds_read_b32, banks (a / 4) mod 32) their buffers' entries i..i+S-1
-  // on distinct banks (2 x FB words per group, a multiple of 32 at FB = 48,
-  // put every group of a half on the same S banks: 8-way on G9-deep's
-  // 4-lane groups, 2-way on P8's 16-lane ones)
-#ifndef TLCG_TREE_FB_PAD  // (0: no padding, A/B)
-#define TLCG_TREE_FB_PAD 1
-#endif
-  constexpr int FBS = FB > 0 ? 2 * FB + (TLCG_TREE_FB_PAD ? ((S % 32) - (2 * FB) % 32 + 32) % 32 : 0) : 1;
+  // (a group stride of S (mod 32) words, so that the groups of a half-wave
+  // read their buffers on distinct banks, measured slower: G9-deep 7.30-7.35
+  // vs 8.01 ms, the padding costs the bitmap pass a workgroup per CU;
+  // profiles/r06_probe_tree_fbpad.jsonl)
+  constexpr int FBS = FB > 0 ? 2 * FB : 1;
   __shared__ uint32_t fbuf[G * FBS];
   int dbase = 0;  // the first position of the depth being inserted (FB)
   // per-depth counts: 32 bits (a workgroup runs far fewer than 2^32 states

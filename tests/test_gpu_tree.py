@@ -323,3 +323,41 @@ def test_tree_closed_store_reads_back_states(jit, monkeypatch):
             assert s in [t for _, t in tlcgpu.host_successors(m, ps)]
     finally:
         ck.close()
+
+
+@pytest.mark.parametrize("jit", ["0", "1"])
+def test_tree_closed_store_last_component(jit, monkeypatch):
+    """W_C12 has 729 components, so the wave kernel's last row of
+    64 is padded (25 components, 39 empty lanes).  The whole last row copies
+    back (padded lanes read as 'no walk'), and the last component's slots hold
+    exactly its reachable states, its initial state first; TLCG_JIT=0: the
+    chunk layout (component ci at ci x 640)"""
+    monkeypatch.setenv("TLCG_JIT", jit)
+    m = model_of(GOLDEN["W_C12"]["constants"])
+    nc = tlcgpu.init_count(m)
+    assert nc % 64 != 0
+    cap = 640  # closed mode's store slots per component (csrc/tree.h, tlcg_treec_640)
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run()
+        assert r.engine == "tree"
+        wave = bool(r.jit_used & 16)
+        assert wave == (jit == "1")
+        ci = nc - 1
+        s0 = tlcgpu.host_init_state(m, ci)
+        seen, todo = set(), [s0]
+        while todo:
+            s = todo.pop()
+            if s not in seen:
+                seen.add(s)
+                todo += [t for _, t in tlcgpu.host_successors(m, s)]
+        n = len(seen)
+        assert n * nc == r.distinct
+        if wave:
+            row = ck.copy_states(ci // 64 * 64 * cap, 64 * cap)  # the last row, padded lanes included
+            stored = row[ci % 64::64][:n]
+        else:
+            stored = ck.copy_states(ci * cap, n)
+        assert set(stored) == seen and stored[0] == s0
+    finally:
+        ck.close()
