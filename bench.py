@@ -608,10 +608,13 @@ def main():
     def tree_kernel_name(jit):
         if open_model:
             return ("tlcg_tree_384 (hipRTC-specialized, " if jit & 1 else "k_tree<384, 512, 4> (") + \
-                "component tree, 4 components per wavefront)"
+                "component tree, 4 components per wavefront, double-hashed LDS tables)"
         if jit & 16:
             return "tlcg_treecw_640 (hipRTC-specialized, component tree closed mode: one code-graph walk " \
                 "per wavefront, lane-interleaved store)"
+        if jit & 128:
+            return "tlcg_treecb_640 (hipRTC-specialized, component tree closed mode: component codes, " \
+                "a bitmap FPSet over the host's perfect hash, 16 components per wavefront)"
         return ("tlcg_treec_640 (hipRTC-specialized, " if jit & 1 else "k_tree<640, 1024, 4, closed> (") + \
             "component tree closed mode: component codes, 4 components per wavefront)"
 

@@ -251,9 +251,11 @@ int tlcg_outdegree(tlcg_ctx* c, uint64_t* hist, int32_t cap, int32_t* n);
  * in it -- each state of each component for a per-lane kernel
  * (component_body.h, component_lane.h), each code state of a walk once for all
  * the walk's M x 64 components for the one-walk-per-wavefront kernel
- * (component_wave.h); the one-rank global engine reports the states of its
+ * (component_wave.h); the component tree counts each component's states
+ * (tree_body.h) or each walk's code states (tree_wave.h) of its last
+ * successful pass; the one-rank global engine reports the states of its
  * expanded levels.  So distinct / expansions is 1 for a per-state kernel and
- * the components per walk for the wave kernel.  -2 for other engines.  (TLC
+ * the components per walk for the wave kernels.  -2 for other engines.  (TLC
  * has no counterpart: its workers expand each state once.) */
 int tlcg_expansions(tlcg_ctx* c, uint64_t* out);
 /* States generated per BFS level: out[0] = the initial states, out[k] = the

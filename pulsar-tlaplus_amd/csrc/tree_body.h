@@ -186,6 +186,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   __syncthreads();
   unsigned flags = 0;
   uint32_t maxn = 0;
+  u64 nexp = 0;  // states this lane's group expanded (its last lane counts them per depth)
   u64 evk = ~0ull;  // this lane's least error key (tree_event_key)
   u64 subtree = 0;  // Producer modelled: the group's component's first message (its subtree), nkv for the root
   // a group's current component and its BFS state (uniform inside the group)
@@ -465,6 +466,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
       for (int off = S / 2; off > 0; off >>= 1) gen += __shfl_xor(gen, off);
     }
     if (have && sub == S - 1 && d < TREE_MAXLV && a.count) {
+      nexp += (u64)(f1 - f0);
       if (d < LV) {
         atomicAdd(&lvl_d[d], (lvl_t)(f1 - f0));
         atomicAdd(&lvl_g[d], (lvl_t)gen);
@@ -487,10 +489,12 @@ __device__ __forceinline__ void tree_body(const TreeArgs& a, const Layout& L) {
   for (int off = 32; off > 0; off >>= 1) maxn = max(maxn, (uint32_t)__shfl_xor(maxn, off));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) evk = min(evk, (u64)__shfl_xor((unsigned long long)evk, off));
+  nexp = wave_sum_u64(nexp);
   if (lane == 0) {
     if (fo) atomicOr(a.flags, fo);
     atomicMax(a.max_n, maxn);
     if (evk != ~0ull) atomicMin(a.event, (unsigned long long)evk);
+    if (nexp && a.expansions) atomicAdd(&a.expansions[a.nstripe > 1 ? blockIdx.x % (unsigned)a.nstripe : 0], nexp);
   }
   __syncthreads();
   const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy

@@ -59,6 +59,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
   for (int i = lane; i < TREE_MAXLV; i += 64) lvl_d[i] = lvl_g[i] = 0;
   unsigned flags = 0;
   uint32_t maxn = 0;
+  u64 nexp = 0;  // code states the walks expanded (lane-uniform)
   u64 evk = ~0ull;  // this lane's least error key
   const u64 nb = (a.n_comp + 63) / 64;
   const int ord_crash = ordinal_of(L, ACT_CRASH, 0);
@@ -256,6 +257,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
         if (in(m)) a.n_out[ci] = (uint32_t)tail;
       }
       if (full && nwalk) flags |= TREE_OVERFLOW;
+      if (nwalk) nexp += (u64)head;  // the walk's code states, expanded once for its components
       maxn = nwalk && (uint32_t)tail > maxn ? (uint32_t)tail : maxn;
       __syncthreads();  // (the next walk clears the table)
     }
@@ -268,6 +270,7 @@ __device__ __forceinline__ void tree_wave_body(const TreeArgs& a, const Layout& 
     if (fo) atomicOr(a.flags, fo);
     atomicMax(a.max_n, maxn);
     if (evk != ~0ull) atomicMin(a.event, (unsigned long long)evk);
+    if (nexp && a.expansions) atomicAdd(&a.expansions[a.nstripe > 1 ? blockIdx.x % (unsigned)a.nstripe : 0], nexp);
   }
   __syncthreads();
   const u64 so = a.nstripe > 1 ? (u64)(blockIdx.x % (unsigned)a.nstripe) * a.stripe : 0;  // this workgroup's copy

@@ -361,3 +361,31 @@ def test_tree_closed_store_last_component(jit, monkeypatch):
         assert set(stored) == seen and stored[0] == s0
     finally:
         ck.close()
+
+
+@pytest.mark.parametrize("case,mode", [("P_published", "auto"), ("W_C12", "perlane"), ("W_C12", "wave")])
+def test_tree_expansions_count(case, mode, monkeypatch):
+    """tlcg_expansions on the component tree: each component's states are
+    expanded once at their depth (tree_body.h; the Producer tree and the closed
+    mode's per-state passes), so distinct / expansions = 1; the closed mode's
+    wave kernel (tree_wave.h) expands each walk's code states once for all its
+    components (W_C12: 557 code states per walk, 729 components)"""
+    if mode == "perlane":
+        monkeypatch.setenv("TLCG_JIT", "1")
+        monkeypatch.setenv("TLCG_TREE_WAVE", "0")
+    elif mode == "wave":
+        monkeypatch.setenv("TLCG_JIT", "1")
+    m = model_of(GOLDEN[case]["constants"])
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run(with_trace=False)
+        assert r.engine == "tree" and r.distinct == GOLDEN[case]["result"]["distinct"]
+        x = ck.expansions()
+        if mode == "wave":
+            assert r.jit_used & 16
+            n = r.distinct // tlcgpu.init_count(m)
+            assert x % n == 0 and 0 < x < r.distinct, (x, n)
+        else:
+            assert x == r.distinct, (x, r.distinct)
+    finally:
+        ck.close()
