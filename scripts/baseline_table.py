@@ -85,8 +85,8 @@ head("G9 + `LatestIsLast` (config 5)", b["g9u"], "component, per lane (`tlcg_com
 glob_row("G9 + `LatestIsLast`", b["g9u"])
 head("G9 + six user invariants", b["g9uall"], "component, per lane (`tlcg_componentp_64`)", True)
 wave_row("G9 + six user invariants", b["g9uall"], "4 x 64 components per walk")
-rows.append("| G9 partition 2 (config 4, round 6) | 8 ranks on one GPU | global, exchange (pull, one wait per level) | 7.3e9 | 141-142 (one context 87; round 5 on another box 123.5-131) | -- | -- | -- | -- |")
-rows.append("| G9 partition 2 (config 4, round 6) | 2 ranks on one GPU | the same | 9.4e9 | 111 (1.28x one context) | -- | -- | -- | -- |")
+rows.append("| G9 partition 2 (config 4, round 6 at HEAD, `profiles/r06_node_final.jsonl`) | 8 ranks on one GPU | global, exchange (pull, one wait per level) | 7.7e9 | 133-136 (1.30x one context, 104 on the same box; earlier this round on another box 141-142 against 87) | -- | -- | -- | -- |")
+rows.append("| G9 partition 2 (config 4, round 6 at HEAD) | 2 ranks on one GPU | the same | 1.05e10 | 99 (0.95x one context) | -- | -- | -- | -- |")
 
 p = os.path.join(ROOT, "BASELINE.md")
 s = open(p).read()
