@@ -363,6 +363,26 @@ bool build_lane_phash(const HostModel& hm, uint32_t* mult, uint32_t* owner) {
   return false;
 }
 
+int lane_ring_entries(const Layout& L) {
+  if (L.producer || code_bits(L) > 16 || L.C > 3) return 16;
+  // component 0's FIFO BFS in the kernel's order (compactor successor, then
+  // BrokerCrash's, each appended when new); the widest queue after an expansion
+  const u128 s0 = init_state<u128>(L, 0);
+  const CodeConsts kc = code_consts(L, comp_msgs_init(L, (u64)s0));
+  std::vector<uint32_t> q{code_encode_w<u128>(L, s0)};
+  std::unordered_set<uint32_t> seen{q[0]};
+  size_t width = 0;
+  for (size_t head = 0; head < q.size(); ++head) {
+    if (q.size() >= 63) return 16;  // (past the pass's capacity: the cascade runs it)
+    ckey t = 0, t2 = 0;
+    int act = 0;
+    if (compactor_step_cb(L, kc, q[head], &t, &act) == 1 && seen.insert(t).second) q.push_back(t);
+    if (crash_step_c(L, q[head], &t2) && seen.insert(t2).second) q.push_back(t2);
+    width = std::max(width, q.size() - (head + 1));
+  }
+  return width + 2 <= 8 ? 8 : 16;
+}
+
 template <typename W>
 std::string format_state(const HostModel& hm, W s) {
   const Layout& L = hm.L;

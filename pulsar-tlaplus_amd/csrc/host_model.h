@@ -74,6 +74,12 @@ bool build_slot_owner(const HostModel& hm, int T, uint32_t mult, uint32_t dmult,
 // multiplier of a fixed sequence that works; false when the component has 63
 // or more states (the pass's capacity) or no multiplier was found
 bool build_lane_phash(const HostModel& hm, uint32_t* mult, uint32_t* owner);
+// the per-lane pass's FIFO ring entries (component_lane.h LANE_R, a hipRTC
+// define): the smallest power of 2 >= 8 whose ring holds component 0's widest
+// queue (the kernel sends a component on to the cascade once tail - head >
+// R - 2 after an expansion), 16 when that does not fit or the model has no
+// per-lane pass.  Depends on the layout alone (component 0's closure).
+int lane_ring_entries(const Layout& L);
 
 // every invariant of the cfg, the user's included: -1, else (index << 1) | is_error
 template <typename W>

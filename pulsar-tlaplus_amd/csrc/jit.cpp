@@ -2,6 +2,7 @@
 // kernel (see jit.h).  The source is the same component_body.h the
 // precompiled kernel uses, plus `constexpr Layout kL = {...}`.
 #include "jit.h"
+#include "host_model.h"
 
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
@@ -69,6 +70,15 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
   if (part == JIT_WAVE_BIG)
     s += "#ifndef TLCG_WAVE_M\n#define TLCG_WAVE_M " + std::to_string(WAVE_M_BIG) +
          "\n#endif\n#ifndef TLCG_WAVE_ATTR\n#define TLCG_WAVE_ATTR __attribute__((amdgpu_waves_per_eu(6)))\n#endif\n";
+  // the per-lane pass's FIFO ring: as few entries as component 0's widest
+  // queue needs (host_model.cpp lane_ring_entries; G9: 8 instead of 16, 1 KB
+  // less LDS and fewer registers: G9 3.49-3.53 -> 3.37-3.43 ms,
+  // profiles/r06_probe_lane_r.jsonl), and 8 waves per SIMD (<= 64 VGPRs) --
+  // both together 3.30 ms; a define in TLCG_JIT_DEFINES wins
+  if (part == JIT_MAIN) {
+    s += "#ifndef TLCG_LANE_R\n#define TLCG_LANE_R " + std::to_string(lane_ring_entries(L)) + "\n#endif\n";
+    if (user.empty()) s += "#ifndef TLCG_LANE_ATTR\n#define TLCG_LANE_ATTR __attribute__((amdgpu_waves_per_eu(8)))\n#endif\n";
+  }
   s += kJitSource;
   s += "\n" + layout_literal(L);
   s += user;
@@ -117,7 +127,10 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
   for (const char* od : {"false", "true"})
     s += std::string("extern \"C\" __global__ __launch_bounds__(64) TLCG_LANE_ATTR void tlcg_componentp") +
          (od[0] == 't' ? "od" : "") + "_64(tlcg::CompArgs a) { tlcg::component_lane_body<64, " + od + ">(a, kL); }\n";
-  s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_384(tlcg::TreeArgs a) "
+  // (TLCG_TREE_ATTR / TLCG_TREECB_ATTR: tuning hooks for the Producer tree's
+  // and the closed tree's bitmap-pass attributes, e.g. amdgpu_waves_per_eu)
+  s += "#ifndef TLCG_TREE_ATTR\n#define TLCG_TREE_ATTR\n#endif\n#ifndef TLCG_TREECB_ATTR\n#define TLCG_TREECB_ATTR\n#endif\n";
+  s += "extern \"C\" __global__ __launch_bounds__(64) TLCG_TREE_ATTR void tlcg_tree_384(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<384, 512, 4>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_tree_1024(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<1024, 2048, 1>(a, kL); }\n";
@@ -129,7 +142,7 @@ std::string program_source(const Layout& L, const std::string& user, int part = 
        "{ tlcg::tree_body<640, 1024, TLCG_TREEC_G, true, " + w + ">(a, kL); }\n";
   // (the same with the bitmap FPSet over the host's perfect hash, tree_body.h BITS)
   s += "#ifndef TLCG_TREECB_G\n#define TLCG_TREECB_G " + std::to_string(TREECB_G) + "\n#endif\n";
-  s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treecb_640(tlcg::TreeArgs a) "
+  s += "extern \"C\" __global__ __launch_bounds__(64) TLCG_TREECB_ATTR void tlcg_treecb_640(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<640, 1024, TLCG_TREECB_G, true, " + w + ", true>(a, kL); }\n";
   s += "extern \"C\" __global__ __launch_bounds__(64) void tlcg_treec_2048(tlcg::TreeArgs a) "
        "{ tlcg::tree_body<2048, 4096, 1, true, " + w + ">(a, kL); }\n";
