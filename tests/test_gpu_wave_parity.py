@@ -144,6 +144,37 @@ def test_lane_pass_runs(case, monkeypatch):
     assert r.engine == "component" and r.jit_used & 32 and not r.jit_used & 8, r.jit_used
 
 
+@pytest.mark.parametrize("ring", ["4", "16"])
+@pytest.mark.parametrize("case", ["S", "V_leak", "V_dup", "R_C2_K2"])
+def test_lane_ring_size(case, ring, monkeypatch):
+    """the per-lane pass's FIFO ring (component_lane.h LANE_R) is sized per
+    layout by the host (host_model.cpp lane_ring_entries: 8 when component 0's
+    widest queue fits); forced to 4, components whose queue outgrows it leave
+    the pass for the cascade (the `full` branch), and to 16 the pre-sizing
+    ring: both with the golden result, error reports included"""
+    set_mode(monkeypatch, "perlane")
+    monkeypatch.setenv("TLCG_JIT_DEFINES", "TLCG_LANE_R=" + ring)
+    m = model_of(GOLDEN[case]["constants"])
+    r = tlcgpu.run(m)
+    check_against_golden(case, r, False)
+    assert r.engine == "component" and r.jit_used & 32, r.jit_used
+
+
+def test_g9_lane_ring_4_cascades_exactly(monkeypatch):
+    """G9 with a 4-entry ring: every component outgrows it and the 32-bit
+    cascade redoes it, counting only the levels the lane pass left open"""
+    set_mode(monkeypatch, "perlane")
+    monkeypatch.setenv("TLCG_JIT_DEFINES", "TLCG_LANE_R=4")
+    m = tlcgpu.Model(**G9)
+    ck = tlcgpu.Checker(m)
+    try:
+        r = ck.run(with_trace=False)
+        assert r.engine == "component" and r.jit_used & 32
+        assert (r.distinct, r.generated, r.depth) == (1_040_187_392, 1_392_508_928, 20)
+    finally:
+        ck.close()
+
+
 @pytest.mark.parametrize("mode", ["default", "perlane", "perlane_body"])
 def test_g9_ledger_leak(mode, monkeypatch):
     """G9 (16^6 components, so the default engine runs the big-model wave
