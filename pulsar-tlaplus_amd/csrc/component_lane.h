@@ -31,9 +31,10 @@
 //     the lanes that close a level at one level are one DPP sum and one LDS
 //     add instead of 64 same-address LDS adds (component_body.h's bank
 //     conflicts), and the loop pays no exec-mask bookkeeping per branch.
-// LDS per 64-lane workgroup: the ring 2 KB (16 entries; a wider frontier
-// sends the component to the cascade), the bits 2 KB, owner 1 KB (vs 13.3 KB
-// for component_body.h), so registers, not LDS, set the occupancy.
+// LDS per 64-lane workgroup: the ring R x 128 B (the host picks R per layout,
+// jit.cpp / host_model.cpp lane_ring_entries: 8 entries, 1 KB, on G9; a wider
+// frontier sends the component to the cascade), the bits 2 KB, owner 1 KB (vs
+// 13.3 KB for component_body.h), so registers, not LDS, set the occupancy.
 #pragma once
 #if !defined(__HIPCC_RTC__)
 #include "component_body.h"
@@ -44,7 +45,7 @@ namespace tlcg {
 #ifndef TLCG_LANE_R
 #define TLCG_LANE_R 16
 #endif
-constexpr int LANE_R = TLCG_LANE_R;  // FIFO ring entries per lane (a power of 2)
+constexpr int LANE_R = TLCG_LANE_R;  // FIFO ring entries per lane (a power of 2; the hipRTC module defines it)
 // the compactor disjunct through its update masks (component_code.h
 // compactor_step_tab: one LDS read and a few bit operations instead of the six
 // candidate successors of compactor_step_cb); 0: compactor_step_cb (A/B)
